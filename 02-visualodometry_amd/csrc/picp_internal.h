@@ -1,0 +1,58 @@
+// picp_internal.h -- device-visible data layout shared by the HIP kernels and the host
+// runtime of libpicp_amd.so.  Not part of the public C-ABI (include/picp_c.h).
+//
+// HBM layout of a PICP batch (DESIGN.md §Data layout):
+//   planes X,Y,Z,U,V : float32 SoA, one plane each, problem p occupies
+//                      [prob.offset, prob.offset + prob.n) of every plane; offsets are
+//                      multiples of 4 floats so every block streams float4 (dwordx4) loads.
+//   PicpProblem[np]  : per-problem constants (camera, gate, damping, loop controls).
+//   int4 blkinfo[nb] : linearize block -> (problem, first item, item count).
+//   PicpState[2][np] : ping-pong per-problem solver state (pose + icp_test loop state).
+//   float part[2][nb][32] : ping-pong per-block partial sums of the normal equations.
+#pragma once
+#include <stdint.h>
+
+#define PICP_BLOCK 256            // threads per linearize block (4 waves of 64)
+#define PICP_NPART 32             // floats per block partial (31 used)
+// partial slot layout
+#define PICP_P_H 0                // 21 upper-triangle entries of H (row-major upper)
+#define PICP_P_B 21               // 6 entries of b
+#define PICP_P_CHI_IN 27
+#define PICP_P_CHI_OUT 28
+#define PICP_P_N_IN 29
+#define PICP_P_N_PROJ 30
+
+struct PicpProblem {
+  int64_t offset;      // first item in the SoA planes (multiple of 4)
+  int32_t n;           // number of correspondences
+  int32_t blk0;        // first linearize block (index into partials) of this problem
+  int32_t nblk;        // number of linearize blocks (>= 1)
+  int32_t rows, cols;  // image size (src/camera.h:43-44)
+  float K[9];          // camera matrix, column-major
+  float threshold;     // kernel threshold (src/picp_solver.h:72)
+  float damping;       // src/picp_solver.h:73
+  int32_t min_inliers; // src/picp_solver.h:74
+  int32_t keep_outliers;
+  int32_t max_rounds;  // exec/icp_test.cpp:88
+  float conv_eps;      // exec/icp_test.cpp:91 (negative: never converge)
+  int32_t pad[2];
+};
+
+// 128-byte per-problem solver state
+struct PicpState {
+  float R[9];          // world-in-camera rotation, column-major
+  float t[3];          // world-in-camera translation
+  float chi_prev;      // icp_test's prevError (exec/icp_test.cpp:89,106)
+  float chi_in;        // stats of the last linearization (chiInliers)
+  float chi_out;       // chiOutliers
+  int32_t n_in;        // numInliers
+  int32_t n_proj;      // correspondences that passed projectPoint
+  int32_t rounds;      // oneRound calls executed
+  int32_t done;        // loop finished (converged, failed or max_rounds)
+  int32_t ok;          // return value of the last oneRound
+  int32_t converged;   // icp_test's convergenceReached
+  int32_t pad[11];
+};
+
+static_assert(sizeof(PicpState) == 128, "PicpState must be 128 B");
+static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");

@@ -1,0 +1,566 @@
+// picp_kernels.hip -- hand-written gfx950 (MI355X / CDNA4) kernels of the PICP hot path.
+//
+//   picp_round_kernel   one Gauss-Newton round of a batch of PICP problems:
+//                       prologue  = finish the previous round (deterministic double reduce of
+//                                   the block partials, damped 6x6 LDL^T solve, v2tEuler
+//                                   left-update, icp_test convergence test);
+//                       body      = linearize: one lane per correspondence, float4 SoA loads,
+//                                   projection + 2x6 Jacobian + chi2 gate in registers,
+//                                   halving-butterfly wave64 reduction of the 31 normal-equation
+//                                   terms, LDS cross-wave sum, one 128 B partial per block.
+//   picp_gather_kernel  IntPairVector gather (image idx, world idx) -> SoA planes.
+//   picp_triangulate_kernel  batched two-view DLT (cv::triangulatePoints replacement).
+//
+// Reference semantics: src/picp_solver.cpp:26-105, src/camera.h:24-36, src/defs.h:100-145,
+// exec/icp_test.cpp:88-107, src/cam.cpp:94-140 (paths relative to the reference root).
+// Memory-bound (20 algorithmic B and ~160 FP32 flop per correspondence-round): no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <stdint.h>
+
+#include "picp_internal.h"
+
+namespace picp {
+
+struct Pose {
+  float r00, r01, r02, r10, r11, r12, r20, r21, r22;
+  float t0, t1, t2;
+};
+
+struct Cam {
+  float k00, k01, k02, k10, k11, k12, k20, k21, k22;
+  float maxx, maxy;  // cols-1, rows-1 (src/camera.h:31,33)
+};
+
+struct Acc {
+  float h[21];  // upper triangle of H, row-major (i<=j)
+  float b[6];
+  float chi_in, chi_out, n_in, n_proj;
+};
+
+// ---------------------------------------------------------------------------------------
+// Per-correspondence math.  The block that decides projectability and the chi2 gate is
+// compiled with FP contraction OFF and evaluates every sum left to right, exactly like the
+// CPU oracle (oracle/picp_oracle.c), so inlier/outlier/skip decisions are bit-identical to
+// the oracle at the same pose.  The Jacobian and accumulation are free to use FMA.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, float thr,
+                                               bool keep, float x, float y, float z, float u,
+                                               float v, bool in_range, Acc& a) {
+  float pc0, pc1, pc2, ph0, ph1, ph2, iz, e0, e1, chi;
+  bool valid;
+  {
+#pragma clang fp contract(off)
+    // src/camera.h:26  pc = R*p + t
+    pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;
+    pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
+    pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
+    // src/camera.h:29  ph = K*pc
+    ph0 = (C.k00 * pc0 + C.k01 * pc1) + C.k02 * pc2;
+    ph1 = (C.k10 * pc0 + C.k11 * pc1) + C.k12 * pc2;
+    ph2 = (C.k20 * pc0 + C.k21 * pc1) + C.k22 * pc2;
+    // src/camera.h:30 / picp_solver.cpp:44: (float)(1.0/(double)z) == correctly rounded
+    // 1.0f/z (double rounding is innocuous for division at 53 >= 2*24+2); hipcc's default
+    // fp32 division is correctly rounded.
+    iz = 1.0f / ph2;
+    const float ix = ph0 * iz;
+    const float iy = ph1 * iz;
+    // src/camera.h:27-28 (z<=0 rejects; NaN passes as in the reference) and :31-34
+    valid = in_range && !(pc2 <= 0.0f) &&
+            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    e0 = ix - u;  // src/picp_solver.cpp:34
+    e1 = iy - v;
+    chi = e0 * e0 + e1 * e1;  // src/picp_solver.cpp:74
+  }
+  // src/picp_solver.cpp:75-89: strict gate, sqrt kernel weight, outliers only with keep
+  const bool outlier = chi > thr;
+  const bool inl = valid && !outlier;
+  const bool use = inl || (valid && keep);
+  const float lambda = outlier ? sqrtf(thr / chi) : 1.0f;
+  const float w = inl ? 1.0f : lambda;
+  a.chi_in += inl ? chi : 0.0f;
+  a.chi_out += (valid && outlier) ? chi : 0.0f;
+  a.n_in += inl ? 1.0f : 0.0f;
+  a.n_proj += valid ? 1.0f : 0.0f;
+  // unused terms are zeroed by select before the Jacobian, so a skipped point (possibly
+  // with an infinite iz) can never inject inf/NaN into H or b
+  iz = use ? iz : 0.0f;
+  pc0 = use ? pc0 : 0.0f;
+  pc1 = use ? pc1 : 0.0f;
+  pc2 = use ? pc2 : 0.0f;
+  ph0 = use ? ph0 : 0.0f;
+  ph1 = use ? ph1 : 0.0f;
+  e0 = use ? e0 : 0.0f;
+  e1 = use ? e1 : 0.0f;
+  // src/picp_solver.cpp:38-52: J = Jp * K * [I | skew(-pc)]
+  const float iz2 = iz * iz;
+  const float jp02 = -ph0 * iz2, jp12 = -ph1 * iz2;
+  const float a00 = iz * C.k00 + jp02 * C.k20;  // (Jp*K)(0,c)
+  const float a01 = iz * C.k01 + jp02 * C.k21;
+  const float a02 = iz * C.k02 + jp02 * C.k22;
+  const float a10 = iz * C.k10 + jp12 * C.k20;  // (Jp*K)(1,c)
+  const float a11 = iz * C.k11 + jp12 * C.k21;
+  const float a12 = iz * C.k12 + jp12 * C.k22;
+  float J0[6], J1[6];
+  J0[0] = a00; J0[1] = a01; J0[2] = a02;
+  J0[3] = a02 * pc1 - a01 * pc2;
+  J0[4] = a00 * pc2 - a02 * pc0;
+  J0[5] = a01 * pc0 - a00 * pc1;
+  J1[0] = a10; J1[1] = a11; J1[2] = a12;
+  J1[3] = a12 * pc1 - a11 * pc2;
+  J1[4] = a10 * pc2 - a12 * pc0;
+  J1[5] = a11 * pc0 - a10 * pc1;
+  float W0[6], W1[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    W0[i] = w * J0[i];
+    W1[i] = w * J1[i];
+  }
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      a.h[k] = fmaf(W0[i], J0[j], fmaf(W1[i], J1[j], a.h[k]));
+      ++k;
+    }
+    a.b[i] = fmaf(W0[i], e0, fmaf(W1[i], e1, a.b[i]));
+  }
+}
+
+// One halving-butterfly step over 2*HALF values: lanes l and l^M exchange the half the
+// other keeps, so the number of live values per lane halves per step (32 -> 1 in five
+// steps, 32 cross-lane moves in total instead of 6*32 for a naive per-value tree).
+template <int M, int HALF>
+__device__ __forceinline__ void bfly(float* v, int lane) {
+  const bool hi = (lane & M) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const float send = hi ? v[i] : v[i + HALF];
+    const float keep = hi ? v[i + HALF] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
+  }
+}
+
+// Sum 32 per-lane values over the 64 lanes of a wave.  Returns, in every lane, the wave
+// total of value index (lane >> 1).
+__device__ __forceinline__ float wave_reduce32(float* v, int lane) {
+  bfly<32, 16>(v, lane);
+  bfly<16, 8>(v, lane);
+  bfly<8, 4>(v, lane);
+  bfly<4, 2>(v, lane);
+  bfly<2, 1>(v, lane);
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+// Damped normal equations -> dx, plain LDL^T (H + damping*I is SPD) in double, fully
+// unrolled so everything stays in registers.  Eigen's LDLT (src/picp_solver.cpp:102) adds
+// diagonal pivoting, which only changes rounding for an SPD matrix; the zero-pivot rule
+// (|d| <= DBL_MIN -> component 0) is Eigen's.
+__device__ __forceinline__ void ldlt6_solve(double A[6][6], const double rhs[6], double x[6]) {
+  double L[6][6], D[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = A[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
+    D[j] = d;
+    const double id = (fabs(d) > 0.0) ? 1.0 / d : 0.0;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double s = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k] * D[k];
+      L[i][j] = s * id;
+    }
+  }
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double s = rhs[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+    y[i] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) y[i] = (fabs(D[i]) > DBL_MIN) ? y[i] / D[i] : 0.0;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+    x[i] = s;
+  }
+}
+
+// src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
+// src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
+__device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
+  float sa, ca, sb, cb, sc, cc;
+  sincosf(dx[3], &sa, &ca);
+  sincosf(dx[4], &sb, &cb);
+  sincosf(dx[5], &sc, &cc);
+  const float Rx[3][3] = {{1.f, 0.f, 0.f}, {0.f, ca, -sa}, {0.f, sa, ca}};
+  const float Ry[3][3] = {{cb, 0.f, sb}, {0.f, 1.f, 0.f}, {-sb, 0.f, cb}};
+  const float Rz[3][3] = {{cc, -sc, 0.f}, {sc, cc, 0.f}, {0.f, 0.f, 1.f}};
+  float Rxy[3][3], Rd[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float s = Rx[i][0] * Ry[0][j];
+      s = s + Rx[i][1] * Ry[1][j];
+      s = s + Rx[i][2] * Ry[2][j];
+      Rxy[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float s = Rxy[i][0] * Rz[0][j];
+      s = s + Rxy[i][1] * Rz[1][j];
+      s = s + Rxy[i][2] * Rz[2][j];
+      Rd[i][j] = s;
+    }
+  float Rn[9], tn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float s = Rd[i][0] * R[j * 3 + 0];
+      s = s + Rd[i][1] * R[j * 3 + 1];
+      s = s + Rd[i][2] * R[j * 3 + 2];
+      Rn[j * 3 + i] = s;
+    }
+    float s = Rd[i][0] * t[0];
+    s = s + Rd[i][1] * t[1];
+    s = s + Rd[i][2] * t[2];
+    tn[i] = s + dx[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = tn[i];
+}
+
+// Finish round (j-1) of problem p from its block partials: H, b, stats -> new state.
+// Runs in one lane; everything is indexed by compile-time constants.
+__device__ void finish_round(const PicpProblem& P, const PicpState& s, const double* tot,
+                             int j, PicpState& ns) {
+  ns = s;
+  ns.chi_in = (float)tot[PICP_P_CHI_IN];
+  ns.chi_out = (float)tot[PICP_P_CHI_OUT];
+  ns.n_in = (int32_t)tot[PICP_P_N_IN];
+  ns.n_proj = (int32_t)tot[PICP_P_N_PROJ];
+  ns.rounds = j;
+  double H[6][6];
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = r; c < 6; ++c) {
+      H[r][c] = tot[PICP_P_H + k];
+      H[c][r] = tot[PICP_P_H + k];
+      ++k;
+    }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) H[r][r] += (double)P.damping;  // src/picp_solver.cpp:96
+  if (ns.n_in < P.min_inliers) {                              // :97-100
+    ns.ok = 0;
+    ns.done = 1;
+    return;
+  }
+  double nb[6], dxd[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) nb[r] = -tot[PICP_P_B + r];
+  ldlt6_solve(H, nb, dxd);  // :102
+  float dx[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) dx[r] = (float)dxd[r];
+  apply_update(dx, ns.R, ns.t);  // :103
+  ns.ok = 1;
+  // exec/icp_test.cpp:99-106
+  const float prev = s.chi_prev, cur = ns.chi_in;
+  const float rel = (prev > 1e-10f) ? fabsf(prev - cur) / prev : 0.0f;
+  if (rel < P.conv_eps) {
+    ns.converged = 1;
+    ns.done = 1;
+  } else {
+    ns.chi_prev = cur;
+  }
+  if (j >= P.max_rounds) ns.done = 1;
+}
+
+}  // namespace picp
+
+using namespace picp;
+
+// Launch j (0 <= j <= R) of the fused R-round solve.  Launch j finishes round j-1 (j>0) and,
+// unless the problem is done, linearizes round j.  With finalize=1 only the finishing part
+// runs, one block per problem.  State and partials ping-pong between launches, so no
+// inter-workgroup synchronisation is ever needed inside a launch: the kernel boundary is the
+// only hand-off.
+extern "C" __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const float* __restrict__ U, const float* __restrict__ V,
+    const PicpProblem* __restrict__ probs, const int4* __restrict__ blkinfo,
+    const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
+    const float* __restrict__ part_in, float* __restrict__ part_out, int j, int finalize) {
+  __shared__ double s_red[8][PICP_NPART];
+  __shared__ float s_wave[PICP_BLOCK / 64][PICP_NPART];
+  __shared__ float s_pose[12];
+  __shared__ int s_go;
+
+  const int tid = threadIdx.x;
+  int p, first = 0, count = 0;
+  if (finalize) {
+    p = blockIdx.x;
+  } else {
+    const int4 bi = blkinfo[blockIdx.x];
+    p = bi.x;
+    first = bi.y;
+    count = bi.z;
+  }
+  const PicpProblem& P = probs[p];
+  const bool leader = finalize || ((int)blockIdx.x == P.blk0);
+
+  if (j == 0) {
+    if (tid < 12) s_pose[tid] = (tid < 9) ? st_in[p].R[tid] : st_in[p].t[tid - 9];
+    if (tid == 0) {
+      PicpState s = st_in[p];
+      s.chi_prev = FLT_MAX;  // exec/icp_test.cpp:89
+      s.chi_in = s.chi_out = 0.0f;
+      s.n_in = s.n_proj = 0;
+      s.rounds = 0;
+      s.done = (P.max_rounds <= 0) ? 1 : 0;
+      s.ok = 1;
+      s.converged = 0;
+      if (leader) st_out[p] = s;
+      s_go = !s.done;
+    }
+  } else {
+    const PicpState& s_in = st_in[p];
+    if (s_in.done) {  // finished earlier: propagate the state through the ping-pong
+      if (leader && tid < 32)
+        reinterpret_cast<int32_t*>(&st_out[p])[tid] =
+            reinterpret_cast<const int32_t*>(&s_in)[tid];
+      return;
+    }
+    // deterministic reduction of the previous round's partials, fixed order, in double
+    const int e = tid & 31, g = tid >> 5;
+    double acc = 0.0;
+    const float* pp = part_in + (size_t)P.blk0 * PICP_NPART + e;
+    for (int b = g; b < P.nblk; b += PICP_BLOCK / 32) acc += (double)pp[(size_t)b * PICP_NPART];
+    s_red[g][e] = acc;
+    __syncthreads();
+    if (tid < 32) {
+      double tsum = 0.0;
+#pragma unroll
+      for (int gg = 0; gg < PICP_BLOCK / 32; ++gg) tsum += s_red[gg][tid];
+      s_red[0][tid] = tsum;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double tot[PICP_NPART];
+#pragma unroll
+      for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_red[0][i];
+      PicpState ns;
+      finish_round(P, s_in, tot, j, ns);
+      if (leader) st_out[p] = ns;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
+      s_go = !ns.done;
+    }
+  }
+  __syncthreads();
+  if (finalize || !s_go) return;
+
+  // ---------------- linearize (src/picp_solver.cpp:56-91) ----------------
+  Pose T;
+  T.r00 = s_pose[0]; T.r10 = s_pose[1]; T.r20 = s_pose[2];
+  T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
+  T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
+  T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
+  Cam C;
+  C.k00 = P.K[0]; C.k10 = P.K[1]; C.k20 = P.K[2];
+  C.k01 = P.K[3]; C.k11 = P.K[4]; C.k21 = P.K[5];
+  C.k02 = P.K[6]; C.k12 = P.K[7]; C.k22 = P.K[8];
+  C.maxx = (float)(P.cols - 1);
+  C.maxy = (float)(P.rows - 1);
+  const float thr = P.threshold;
+  const bool keep = P.keep_outliers != 0;
+
+  Acc a;
+#pragma unroll
+  for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
+  a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
+
+  const int64_t base = P.offset + first;
+  for (int c = tid * 4; c < count; c += PICP_BLOCK * 4) {
+    const float4 x4 = *reinterpret_cast<const float4*>(X + base + c);
+    const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c);
+    const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c);
+    const float4 u4 = *reinterpret_cast<const float4*>(U + base + c);
+    const float4 v4 = *reinterpret_cast<const float4*>(V + base + c);
+    const int rem = count - c;
+    accumulate_one(T, C, thr, keep, x4.x, y4.x, z4.x, u4.x, v4.x, rem > 0, a);
+    accumulate_one(T, C, thr, keep, x4.y, y4.y, z4.y, u4.y, v4.y, rem > 1, a);
+    accumulate_one(T, C, thr, keep, x4.z, y4.z, z4.z, u4.z, v4.z, rem > 2, a);
+    accumulate_one(T, C, thr, keep, x4.w, y4.w, z4.w, u4.w, v4.w, rem > 3, a);
+  }
+
+  float v[PICP_NPART];
+#pragma unroll
+  for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
+  v[PICP_P_CHI_IN] = a.chi_in;
+  v[PICP_P_CHI_OUT] = a.chi_out;
+  v[PICP_P_N_IN] = a.n_in;
+  v[PICP_P_N_PROJ] = a.n_proj;
+  v[31] = 0.0f;
+  const int lane = tid & 63, wave = tid >> 6;
+  const float wsum = wave_reduce32(v, lane);
+  if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
+  __syncthreads();
+  if (tid < PICP_NPART) {
+    float s = s_wave[0][tid];
+#pragma unroll
+    for (int w = 1; w < PICP_BLOCK / 64; ++w) s += s_wave[w][tid];
+    part_out[(size_t)blockIdx.x * PICP_NPART + tid] = s;
+  }
+}
+
+// IntPairVector gather: pairs[k] = (image idx, world idx) (src/picp_solver.cpp:65-66).
+extern "C" __global__ void picp_gather_kernel(const float* __restrict__ world,
+                                              const float* __restrict__ image,
+                                              const int2* __restrict__ pairs, int64_t m,
+                                              float* __restrict__ X, float* __restrict__ Y,
+                                              float* __restrict__ Z, float* __restrict__ U,
+                                              float* __restrict__ V, int64_t off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int2 pr = pairs[i];
+  X[off + i] = world[3 * (int64_t)pr.y + 0];
+  Y[off + i] = world[3 * (int64_t)pr.y + 1];
+  Z[off + i] = world[3 * (int64_t)pr.y + 2];
+  U[off + i] = image[2 * (int64_t)pr.x + 0];
+  V[off + i] = image[2 * (int64_t)pr.x + 1];
+}
+
+// Batched two-view DLT (cv::triangulatePoints as called from src/cam.cpp:115, then
+// convertPointsFromHomogeneous :118).  One lane per point; A (4x4) in double, right singular
+// vector of the smallest singular value by one-sided (Hestenes) Jacobi with a fixed sweep
+// count, all indices compile-time so A and V live in registers.
+extern "C" __global__ void picp_triangulate_kernel(const float* __restrict__ P1,
+                                                   const float* __restrict__ P2,
+                                                   const float2* __restrict__ uv1,
+                                                   const float2* __restrict__ uv2, int64_t q,
+                                                   float* __restrict__ xyz) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q) return;
+  double A[4][4], Vm[4][4];
+  const float2 a = uv1[i], b = uv2[i];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    A[0][k] = (double)a.x * (double)P1[8 + k] - (double)P1[0 + k];
+    A[1][k] = (double)a.y * (double)P1[8 + k] - (double)P1[4 + k];
+    A[2][k] = (double)b.x * (double)P2[8 + k] - (double)P2[0 + k];
+    A[3][k] = (double)b.y * (double)P2[8 + k] - (double)P2[4 + k];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) Vm[r][c] = (r == c) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 10; ++sweep) {
+#pragma unroll
+    for (int pq = 0; pq < 6; ++pq) {
+      const int p = (pq < 3) ? 0 : ((pq < 5) ? 1 : 2);
+      const int qq = (pq < 3) ? pq + 1 : ((pq < 5) ? pq - 1 : 3);
+      double alpha = 0.0, beta = 0.0, gamma = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        alpha += A[k][p] * A[k][p];
+        beta += A[k][qq] * A[k][qq];
+        gamma += A[k][p] * A[k][qq];
+      }
+      if (fabs(gamma) > 1e-300 && fabs(gamma) > 1e-17 * sqrt(alpha * beta)) {
+        const double zeta = (beta - alpha) / (2.0 * gamma);
+        const double t = ((zeta >= 0.0) ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t);
+        const double s = c * t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const double akp = A[k][p], akq = A[k][qq];
+          A[k][p] = c * akp - s * akq;
+          A[k][qq] = s * akp + c * akq;
+          const double vkp = Vm[k][p], vkq = Vm[k][qq];
+          Vm[k][p] = c * vkp - s * vkq;
+          Vm[k][qq] = s * vkp + c * vkq;
+        }
+      }
+    }
+  }
+  double nrm[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) nrm[c] = A[0][c] * A[0][c] + A[1][c] * A[1][c] + A[2][c] * A[2][c] + A[3][c] * A[3][c];
+  double best = nrm[0];
+  double v0 = Vm[0][0], v1 = Vm[1][0], v2 = Vm[2][0], v3 = Vm[3][0];
+#pragma unroll
+  for (int c = 1; c < 4; ++c) {
+    const bool take = nrm[c] < best;
+    best = take ? nrm[c] : best;
+    v0 = take ? Vm[0][c] : v0;
+    v1 = take ? Vm[1][c] : v1;
+    v2 = take ? Vm[2][c] : v2;
+    v3 = take ? Vm[3][c] : v3;
+  }
+  // points4D is float; convertPointsFromHomogeneous in float, scale 1 when |w| <= FLT_EPSILON
+  const float X4 = (float)v0, Y4 = (float)v1, Z4 = (float)v2, W4 = (float)v3;
+  const float scale = (fabsf(W4) > FLT_EPSILON) ? 1.0f / W4 : 1.0f;
+  xyz[3 * i + 0] = X4 * scale;
+  xyz[3 * i + 1] = Y4 * scale;
+  xyz[3 * i + 2] = Z4 * scale;
+}
+
+// ------------------------------- host launch wrappers -------------------------------
+// (called by picp_runtime.cpp; every shape/grid assumption is checked there first)
+extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, const float* X,
+                                        const float* Y, const float* Z, const float* U,
+                                        const float* V, const PicpProblem* probs,
+                                        const int4* blkinfo, const PicpState* st_in,
+                                        PicpState* st_out, const float* part_in,
+                                        float* part_out, int j, int finalize) {
+  if (grid <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(picp_round_kernel, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U,
+                     V, probs, blkinfo, st_in, st_out, part_in, part_out, j, finalize);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
+                                         const float* image, const int2* pairs, int64_t m,
+                                         float* X, float* Y, float* Z, float* U, float* V,
+                                         int64_t off) {
+  if (m <= 0) return hipSuccess;
+  const int threads = 256;
+  const int64_t grid = (m + threads - 1) / threads;
+  hipLaunchKernelGGL(picp_gather_kernel, dim3((unsigned)grid), dim3(threads), 0, stream, world,
+                     image, pairs, m, X, Y, Z, U, V, off);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t picp_launch_triangulate(hipStream_t stream, const float* P1,
+                                              const float* P2, const float2* uv1,
+                                              const float2* uv2, int64_t q, float* xyz) {
+  if (q <= 0) return hipSuccess;
+  const int threads = 128;
+  const int64_t grid = (q + threads - 1) / threads;
+  hipLaunchKernelGGL(picp_triangulate_kernel, dim3((unsigned)grid), dim3(threads), 0, stream,
+                     P1, P2, uv1, uv2, q, xyz);
+  return hipGetLastError();
+}

@@ -1,0 +1,854 @@
+// picp_runtime.cpp -- host runtime behind the C-ABI (include/picp_c.h).
+//
+// Owns device memory, the HIP stream of each handle, the block partition of a batch and the
+// hipGraph that replays the fused R-round solve (1 memcpy node + R linearize launches +
+// 1 finalize launch).  No torch, no host fallback: every compute entry point runs the HIP
+// kernels of picp_kernels.hip or fails with PICP_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "picp_c.h"
+#include "picp_internal.h"
+
+extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, const float* X,
+                                        const float* Y, const float* Z, const float* U,
+                                        const float* V, const PicpProblem* probs,
+                                        const int4* blkinfo, const PicpState* st_in,
+                                        PicpState* st_out, const float* part_in,
+                                        float* part_out, int j, int finalize);
+extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
+                                         const float* image, const int2* pairs, int64_t m,
+                                         float* X, float* Y, float* Z, float* U, float* V,
+                                         int64_t off);
+extern "C" hipError_t picp_launch_triangulate(hipStream_t stream, const float* P1,
+                                              const float* P2, const float2* uv1,
+                                              const float2* uv2, int64_t q, float* xyz);
+
+// ------------------------------------------------------------------------------------
+// error plumbing
+// ------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return set_err(e_ == hipErrorOutOfMemory ? PICP_ERR_NOMEM : PICP_ERR_DEVICE,          \
+                     "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,       \
+                     __LINE__);                                                             \
+  } while (0)
+
+#define CHECK_ARG(cond, msg)                                                                \
+  do {                                                                                      \
+    if (!(cond)) return set_err(PICP_ERR_ARG, "%s", msg);                                   \
+  } while (0)
+
+extern "C" const char* picp_last_error(void) { return g_err.c_str(); }
+extern "C" int picp_abi_version(void) { return PICP_ABI_VERSION; }
+
+extern "C" void picp_params_default(picp_params* p) {
+  if (!p) return;
+  p->threshold = 1000.0f;  // src/picp_solver.cpp:14
+  p->damping = 1.0f;       // src/picp_solver.cpp:11
+  p->min_inliers = 0;      // src/picp_solver.cpp:12
+  p->keep_outliers = 0;    // exec/icp_test.cpp:95
+  p->max_rounds = 50;      // exec/icp_test.cpp:88
+  p->conv_eps = 1e-5f;     // exec/icp_test.cpp:91
+}
+
+extern "C" int picp_device_count(int* n) {
+  CHECK_ARG(n, "picp_device_count: null output");
+  int c = 0;
+  HIP_TRY(hipGetDeviceCount(&c));
+  *n = c;
+  return PICP_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// pose helpers (column-major 4x4 <-> state R(col-major 3x3), t)
+// ------------------------------------------------------------------------------------
+static void pose_to_state(const float T[16], PicpState& s) {
+  for (int j = 0; j < 3; ++j)
+    for (int i = 0; i < 3; ++i) s.R[j * 3 + i] = T[j * 4 + i];
+  for (int i = 0; i < 3; ++i) s.t[i] = T[12 + i];
+}
+
+static void state_to_pose(const PicpState& s, float T[16]) {
+  memset(T, 0, 16 * sizeof(float));
+  for (int j = 0; j < 3; ++j)
+    for (int i = 0; i < 3; ++i) T[j * 4 + i] = s.R[j * 3 + i];
+  for (int i = 0; i < 3; ++i) T[12 + i] = s.t[i];
+  T[15] = 1.0f;
+}
+
+static void state_to_stats(const PicpState& s, picp_stats& st) {
+  st.chi_in = s.chi_in;
+  st.chi_out = s.chi_out;
+  st.n_in = s.n_in;
+  st.ok = s.ok;
+  st.rounds = s.rounds;
+  st.converged = s.converged;
+  st.n_projected = s.n_proj;
+  st.reserved = 0;
+}
+
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// ------------------------------------------------------------------------------------
+// batch
+// ------------------------------------------------------------------------------------
+struct picp_batch {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int np = 0;
+  int rows = 0, cols = 0;
+  float K[9];
+  std::vector<int64_t> offs;   // user correspondence offsets (np+1)
+  std::vector<int64_t> plane_off;  // per problem offset into the SoA planes (mult. of 4)
+  int64_t total = 0;           // correspondences
+  int64_t plane_len = 0;       // padded plane length (floats)
+  int64_t plane_cap = 0;       // allocated plane length
+  float* planes = nullptr;     // 5 * plane_cap floats: X | Y | Z | U | V
+  int nblk = 0;                // linearize blocks per launch
+  int nblk_cap = 0;
+  int np_cap = 0;
+  std::vector<PicpProblem> probs_h;
+  std::vector<int4> blk_h;
+  PicpProblem* probs_d = nullptr;
+  int4* blk_d = nullptr;
+  PicpState* init_d = nullptr;
+  PicpState* st_d[2] = {nullptr, nullptr};
+  float* part_d[2] = {nullptr, nullptr};
+  PicpState* st_pinned = nullptr;  // np_cap states
+  std::vector<PicpState> init_h;
+  std::vector<PicpState> result_h;
+  bool probs_dirty = true;
+  picp_params params;
+  // graph cache
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  int g_rounds = -1;
+  int last_rounds = 0;  // R of the last solve (final state in st_d[R&1])
+
+  float* X() const { return planes; }
+  float* Y() const { return planes + plane_cap; }
+  float* Z() const { return planes + 2 * plane_cap; }
+  float* U() const { return planes + 3 * plane_cap; }
+  float* V() const { return planes + 4 * plane_cap; }
+};
+
+static void drop_graph(picp_batch* b) {
+  if (b->gexec) hipGraphExecDestroy(b->gexec);
+  if (b->graph) hipGraphDestroy(b->graph);
+  b->gexec = nullptr;
+  b->graph = nullptr;
+  b->g_rounds = -1;
+}
+
+static int items_per_block(int64_t total) {
+  const char* env = getenv("PICP_ITEMS_PER_BLOCK");
+  if (env) {
+    int v = atoi(env);
+    if (v >= 4) return (int)round_up(v, 4);
+  }
+  // one float4 per lane per block for latency-bound single frames; deeper per-lane
+  // accumulation for large (HBM-streaming) batches to amortise the block reduction
+  if (total >= (int64_t)8 << 20) return PICP_BLOCK * 4 * 4;
+  if (total >= (int64_t)2 << 20) return PICP_BLOCK * 4 * 2;
+  return PICP_BLOCK * 4;
+}
+
+// (Re)build the partition for correspondence offsets `offs` (np+1 entries).
+static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
+  CHECK_ARG(np >= 1, "batch: n_problems must be >= 1");
+  for (int i = 0; i < np; ++i)
+    CHECK_ARG(offs[i + 1] >= offs[i] && offs[0] == 0, "batch: corr_offsets must be a prefix sum from 0");
+  b->np = np;
+  b->offs.assign(offs, offs + np + 1);
+  b->total = offs[np];
+  const int ipb = items_per_block(b->total);
+  b->plane_off.resize(np);
+  int64_t pos = 0;
+  int nblk = 0;
+  for (int i = 0; i < np; ++i) {
+    b->plane_off[i] = pos;
+    const int64_t n = offs[i + 1] - offs[i];
+    CHECK_ARG(n <= INT32_MAX, "batch: a problem has more than 2^31-1 correspondences");
+    pos = round_up(pos + n, 4);
+    nblk += (int)std::max<int64_t>(1, (n + ipb - 1) / ipb);
+  }
+  b->plane_len = std::max<int64_t>(pos, 4);
+  b->nblk = nblk;
+  hipError_t e;
+  HIP_TRY(hipSetDevice(b->device));
+  if (b->plane_len > b->plane_cap) {
+    if (b->planes) hipFree(b->planes);
+    b->planes = nullptr;
+    const int64_t cap = round_up(b->plane_len, 1024);
+    e = hipMalloc(&b->planes, (size_t)cap * 5 * sizeof(float));
+    if (e != hipSuccess) return set_err(PICP_ERR_NOMEM, "hipMalloc planes (%lld floats): %s", (long long)cap * 5, hipGetErrorString(e));
+    HIP_TRY(hipMemsetAsync(b->planes, 0, (size_t)cap * 5 * sizeof(float), b->stream));
+    b->plane_cap = cap;
+  }
+  if (nblk > b->nblk_cap) {
+    if (b->blk_d) hipFree(b->blk_d);
+    for (int k = 0; k < 2; ++k) if (b->part_d[k]) hipFree(b->part_d[k]);
+    b->blk_d = nullptr; b->part_d[0] = b->part_d[1] = nullptr;
+    HIP_TRY(hipMalloc(&b->blk_d, (size_t)nblk * sizeof(int4)));
+    for (int k = 0; k < 2; ++k) HIP_TRY(hipMalloc(&b->part_d[k], (size_t)nblk * PICP_NPART * sizeof(float)));
+    b->nblk_cap = nblk;
+  }
+  if (np > b->np_cap) {
+    if (b->probs_d) hipFree(b->probs_d);
+    if (b->init_d) hipFree(b->init_d);
+    for (int k = 0; k < 2; ++k) if (b->st_d[k]) hipFree(b->st_d[k]);
+    if (b->st_pinned) hipHostFree(b->st_pinned);
+    b->probs_d = nullptr; b->init_d = nullptr; b->st_d[0] = b->st_d[1] = nullptr; b->st_pinned = nullptr;
+    HIP_TRY(hipMalloc(&b->probs_d, (size_t)np * sizeof(PicpProblem)));
+    HIP_TRY(hipMalloc(&b->init_d, (size_t)np * sizeof(PicpState)));
+    for (int k = 0; k < 2; ++k) {
+      HIP_TRY(hipMalloc(&b->st_d[k], (size_t)np * sizeof(PicpState)));
+      HIP_TRY(hipMemsetAsync(b->st_d[k], 0, (size_t)np * sizeof(PicpState), b->stream));
+    }
+    HIP_TRY(hipHostMalloc((void**)&b->st_pinned, (size_t)np * sizeof(PicpState), hipHostMallocDefault));
+    b->np_cap = np;
+  }
+  // block table
+  b->blk_h.resize(nblk);
+  b->probs_h.resize(np);
+  int blk = 0;
+  for (int i = 0; i < np; ++i) {
+    const int64_t n = offs[i + 1] - offs[i];
+    PicpProblem& P = b->probs_h[i];
+    memset(&P, 0, sizeof(P));
+    P.offset = b->plane_off[i];
+    P.n = (int32_t)n;
+    P.blk0 = blk;
+    const int nb = (int)std::max<int64_t>(1, (n + ipb - 1) / ipb);
+    P.nblk = nb;
+    for (int k = 0; k < nb; ++k) {
+      const int64_t first = (int64_t)k * ipb;
+      const int64_t cnt = std::max<int64_t>(0, std::min<int64_t>(ipb, n - first));
+      b->blk_h[blk + k] = make_int4(i, (int)first, (int)cnt, 0);
+    }
+    blk += nb;
+  }
+  HIP_TRY(hipMemcpyAsync(b->blk_d, b->blk_h.data(), (size_t)nblk * sizeof(int4), hipMemcpyHostToDevice, b->stream));
+  // identity initial poses by default
+  b->init_h.assign(np, PicpState{});
+  for (int i = 0; i < np; ++i) {
+    memset(&b->init_h[i], 0, sizeof(PicpState));
+    b->init_h[i].R[0] = b->init_h[i].R[4] = b->init_h[i].R[8] = 1.0f;
+  }
+  HIP_TRY(hipMemcpyAsync(b->init_d, b->init_h.data(), (size_t)np * sizeof(PicpState), hipMemcpyHostToDevice, b->stream));
+  b->result_h.assign(np, PicpState{});
+  b->probs_dirty = true;
+  drop_graph(b);
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return PICP_OK;
+}
+
+static int batch_upload_params(picp_batch* b, const picp_params* prm) {
+  CHECK_ARG(prm, "null params");
+  CHECK_ARG(prm->max_rounds >= 0 && prm->max_rounds <= 100000, "params.max_rounds out of range");
+  CHECK_ARG(!(prm->threshold != prm->threshold), "params.threshold is NaN");
+  const bool same = !b->probs_dirty && memcmp(&b->params, prm, sizeof(picp_params)) == 0;
+  if (same) return PICP_OK;
+  for (int i = 0; i < b->np; ++i) {
+    PicpProblem& P = b->probs_h[i];
+    P.rows = b->rows;
+    P.cols = b->cols;
+    memcpy(P.K, b->K, sizeof(P.K));
+    P.threshold = prm->threshold;
+    P.damping = prm->damping;
+    P.min_inliers = prm->min_inliers;
+    P.keep_outliers = prm->keep_outliers ? 1 : 0;
+    P.max_rounds = prm->max_rounds;
+    P.conv_eps = prm->conv_eps;
+  }
+  HIP_TRY(hipMemcpyAsync(b->probs_d, b->probs_h.data(), (size_t)b->np * sizeof(PicpProblem), hipMemcpyHostToDevice, b->stream));
+  b->params = *prm;
+  b->probs_dirty = false;
+  return PICP_OK;
+}
+
+// Enqueue the R+1 launches (plus the initial-state copy) of a fused solve on the stream.
+static hipError_t enqueue_solve(picp_batch* b, int R) {
+  hipError_t e = hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState),
+                                hipMemcpyDeviceToDevice, b->stream);
+  if (e != hipSuccess) return e;
+  for (int j = 0; j <= R; ++j) {
+    const int fin = (j == R) ? 1 : 0;
+    const int grid = fin ? b->np : b->nblk;
+    e = picp_launch_round(b->stream, grid, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d,
+                          b->blk_d, b->st_d[(j + 1) & 1], b->st_d[j & 1], b->part_d[(j + 1) & 1],
+                          b->part_d[j & 1], j, fin);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+static int ensure_graph(picp_batch* b, int R) {
+  if (b->gexec && b->g_rounds == R) return PICP_OK;
+  drop_graph(b);
+  HIP_TRY(hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal));
+  hipError_t e = enqueue_solve(b, R);
+  hipGraph_t g = nullptr;
+  hipError_t e2 = hipStreamEndCapture(b->stream, &g);
+  if (e != hipSuccess) { if (g) hipGraphDestroy(g); return set_err(PICP_ERR_DEVICE, "capture: %s", hipGetErrorString(e)); }
+  if (e2 != hipSuccess) return set_err(PICP_ERR_DEVICE, "end capture: %s", hipGetErrorString(e2));
+  b->graph = g;
+  HIP_TRY(hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0));
+  b->g_rounds = R;
+  return PICP_OK;
+}
+
+static int batch_solve_async(picp_batch* b, const picp_params* prm) {
+  HIP_TRY(hipSetDevice(b->device));
+  int rc = batch_upload_params(b, prm);
+  if (rc) return rc;
+  const int R = prm->max_rounds;
+  rc = ensure_graph(b, R);
+  if (rc) return rc;
+  HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
+  b->last_rounds = R;
+  return PICP_OK;
+}
+
+static int batch_read_results(picp_batch* b) {
+  const int R = b->last_rounds;
+  HIP_TRY(hipMemcpyAsync(b->st_pinned, b->st_d[R & 1], (size_t)b->np * sizeof(PicpState),
+                         hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  memcpy(b->result_h.data(), b->st_pinned, (size_t)b->np * sizeof(PicpState));
+  return PICP_OK;
+}
+
+static int batch_create(picp_batch** out, int device, int np, const int64_t* offs, int rows,
+                        int cols, const float K[9]) {
+  CHECK_ARG(out && offs && K, "picp_batch_create: null argument");
+  CHECK_ARG(rows > 0 && cols > 0, "picp_batch_create: rows/cols must be positive");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  CHECK_ARG(device >= 0 && device < ndev, "picp_batch_create: no such HIP device");
+  picp_batch* b = new picp_batch();
+  b->device = device;
+  b->rows = rows;
+  b->cols = cols;
+  memcpy(b->K, K, sizeof(b->K));
+  picp_params_default(&b->params);
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete b;
+    return set_err(PICP_ERR_DEVICE, "stream create: %s", hipGetErrorString(e));
+  }
+  int rc = batch_layout(b, offs, np);
+  if (rc) {
+    picp_batch_destroy(b);
+    return rc;
+  }
+  *out = b;
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_create(picp_batch_t** out, int device, int n_problems,
+                                 const int64_t* corr_offsets, int rows, int cols,
+                                 const float K[9]) {
+  return batch_create(out, device, n_problems, corr_offsets, rows, cols, K);
+}
+
+extern "C" int picp_batch_destroy(picp_batch_t* b) {
+  if (!b) return PICP_OK;
+  hipSetDevice(b->device);
+  if (b->stream) hipStreamSynchronize(b->stream);
+  drop_graph(b);
+  if (b->planes) hipFree(b->planes);
+  if (b->blk_d) hipFree(b->blk_d);
+  if (b->probs_d) hipFree(b->probs_d);
+  if (b->init_d) hipFree(b->init_d);
+  for (int k = 0; k < 2; ++k) {
+    if (b->st_d[k]) hipFree(b->st_d[k]);
+    if (b->part_d[k]) hipFree(b->part_d[k]);
+  }
+  if (b->st_pinned) hipHostFree(b->st_pinned);
+  if (b->stream) hipStreamDestroy(b->stream);
+  delete b;
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_set_data(picp_batch_t* b, const float* xyz, const float* uv) {
+  CHECK_ARG(b && (b->total == 0 || (xyz && uv)), "picp_batch_set_data: null argument");
+  HIP_TRY(hipSetDevice(b->device));
+  std::vector<float> host((size_t)b->plane_len * 5, 0.0f);
+  float* hx = host.data();
+  float* hy = hx + b->plane_len;
+  float* hz = hy + b->plane_len;
+  float* hu = hz + b->plane_len;
+  float* hv = hu + b->plane_len;
+  for (int i = 0; i < b->np; ++i) {
+    const int64_t n = b->offs[i + 1] - b->offs[i], src = b->offs[i], dst = b->plane_off[i];
+    for (int64_t k = 0; k < n; ++k) {
+      hx[dst + k] = xyz[3 * (src + k) + 0];
+      hy[dst + k] = xyz[3 * (src + k) + 1];
+      hz[dst + k] = xyz[3 * (src + k) + 2];
+      hu[dst + k] = uv[2 * (src + k) + 0];
+      hv[dst + k] = uv[2 * (src + k) + 1];
+    }
+  }
+  for (int c = 0; c < 5; ++c)
+    HIP_TRY(hipMemcpyAsync(b->planes + (size_t)c * b->plane_cap, host.data() + (size_t)c * b->plane_len,
+                           (size_t)b->plane_len * sizeof(float), hipMemcpyHostToDevice, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_set_data_device(picp_batch_t* b, const float* dx, const float* dy,
+                                          const float* dz, const float* du, const float* dv) {
+  CHECK_ARG(b && (b->total == 0 || (dx && dy && dz && du && dv)), "picp_batch_set_data_device: null argument");
+  HIP_TRY(hipSetDevice(b->device));
+  const float* src[5] = {dx, dy, dz, du, dv};
+  for (int i = 0; i < b->np; ++i) {
+    const int64_t n = b->offs[i + 1] - b->offs[i];
+    if (n == 0) continue;
+    for (int c = 0; c < 5; ++c)
+      HIP_TRY(hipMemcpyAsync(b->planes + (size_t)c * b->plane_cap + b->plane_off[i], src[c] + b->offs[i],
+                             (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, b->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_set_poses(picp_batch_t* b, const float* T) {
+  CHECK_ARG(b && T, "picp_batch_set_poses: null argument");
+  HIP_TRY(hipSetDevice(b->device));
+  for (int i = 0; i < b->np; ++i) pose_to_state(T + 16 * (size_t)i, b->init_h[i]);
+  HIP_TRY(hipMemcpyAsync(b->init_d, b->init_h.data(), (size_t)b->np * sizeof(PicpState), hipMemcpyHostToDevice, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_get_poses(picp_batch_t* b, float* T) {
+  CHECK_ARG(b && T, "picp_batch_get_poses: null argument");
+  for (int i = 0; i < b->np; ++i) state_to_pose(b->result_h[i], T + 16 * (size_t)i);
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_get_stats(picp_batch_t* b, picp_stats* st) {
+  CHECK_ARG(b && st, "picp_batch_get_stats: null argument");
+  for (int i = 0; i < b->np; ++i) state_to_stats(b->result_h[i], st[i]);
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_solve_async(picp_batch_t* b, const picp_params* prm) {
+  CHECK_ARG(b, "picp_batch_solve_async: null batch");
+  return batch_solve_async(b, prm);
+}
+
+extern "C" int picp_batch_sync(picp_batch_t* b) {
+  CHECK_ARG(b, "picp_batch_sync: null batch");
+  HIP_TRY(hipSetDevice(b->device));
+  return batch_read_results(b);
+}
+
+extern "C" int picp_batch_solve(picp_batch_t* b, const picp_params* prm) {
+  CHECK_ARG(b, "picp_batch_solve: null batch");
+  int rc = batch_solve_async(b, prm);
+  if (rc) return rc;
+  return batch_read_results(b);
+}
+
+extern "C" int picp_batch_info(picp_batch_t* b, int64_t* total, int* nblk) {
+  CHECK_ARG(b, "picp_batch_info: null batch");
+  if (total) *total = b->total;
+  if (nblk) *nblk = b->nblk;
+  return PICP_OK;
+}
+
+extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps,
+                               float* total_ms, float kernel_us[2]) {
+  CHECK_ARG(b && prm && reps > 0, "picp_batch_time: bad argument");
+  HIP_TRY(hipSetDevice(b->device));
+  int rc = batch_upload_params(b, prm);
+  if (rc) return rc;
+  const int R = prm->max_rounds;
+  rc = ensure_graph(b, R);
+  if (rc) return rc;
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, b->stream));
+  for (int r = 0; r < reps; ++r) HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
+  HIP_TRY(hipEventRecord(e1, b->stream));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.0f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  if (total_ms) *total_ms = ms;
+  b->last_rounds = R;
+  if (kernel_us) {
+    // instrumented pass: an event pair around every launch of the same solve
+    std::vector<hipEvent_t> ev((size_t)(R + 2));
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    double lin_us = 0.0, fin_us = 0.0;
+    int lin_n = 0, fin_n = 0;
+    const int ireps = std::max(1, std::min(reps, 5));
+    for (int r = 0; r < ireps; ++r) {
+      HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
+      for (int j = 0; j <= R; ++j) {
+        const int fin = (j == R) ? 1 : 0;
+        HIP_TRY(hipEventRecord(ev[j], b->stream));
+        HIP_TRY(picp_launch_round(b->stream, fin ? b->np : b->nblk, b->X(), b->Y(), b->Z(), b->U(), b->V(),
+                                  b->probs_d, b->blk_d, b->st_d[(j + 1) & 1], b->st_d[j & 1],
+                                  b->part_d[(j + 1) & 1], b->part_d[j & 1], j, fin));
+      }
+      HIP_TRY(hipEventRecord(ev[R + 1], b->stream));
+      HIP_TRY(hipEventSynchronize(ev[R + 1]));
+      for (int j = 0; j <= R; ++j) {
+        float t = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&t, ev[j], ev[j + 1]));
+        if (j == R) { fin_us += 1000.0 * t; ++fin_n; }
+        else { lin_us += 1000.0 * t; ++lin_n; }
+      }
+    }
+    for (auto& e : ev) hipEventDestroy(e);
+    kernel_us[0] = lin_n ? (float)(lin_us / lin_n) : 0.0f;
+    kernel_us[1] = fin_n ? (float)(fin_us / fin_n) : 0.0f;
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return batch_read_results(b);
+}
+
+// ------------------------------------------------------------------------------------
+// single-problem handle (the pr::PICPSolver drop-in)
+// ------------------------------------------------------------------------------------
+struct picp_handle {
+  picp_batch* b = nullptr;
+  float* world_d = nullptr;
+  int64_t n_world = 0, cap_world = 0;
+  float* image_d = nullptr;
+  int64_t n_image = 0, cap_image = 0;
+  int2* pairs_d = nullptr;
+  int64_t cap_pairs = 0;
+  std::vector<int32_t> pairs_h;  // cached copy of the current correspondences
+  int64_t m = -1;                // -1: none set
+  bool have_points = false;
+  bool gathered = false;
+  float pose[16];
+};
+
+static void identity16(float T[16]) {
+  memset(T, 0, 16 * sizeof(float));
+  T[0] = T[5] = T[10] = T[15] = 1.0f;
+}
+
+extern "C" int picp_create(picp_t** out, int device, int rows, int cols, const float K[9]) {
+  CHECK_ARG(out && K, "picp_create: null argument");
+  picp_handle* h = new picp_handle();
+  identity16(h->pose);
+  const int64_t offs[2] = {0, 0};
+  int rc = batch_create(&h->b, device, 1, offs, rows, cols, K);
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return PICP_OK;
+}
+
+extern "C" int picp_destroy(picp_t* h) {
+  if (!h) return PICP_OK;
+  if (h->b) {
+    hipSetDevice(h->b->device);
+    hipStreamSynchronize(h->b->stream);
+  }
+  if (h->world_d) hipFree(h->world_d);
+  if (h->image_d) hipFree(h->image_d);
+  if (h->pairs_d) hipFree(h->pairs_d);
+  picp_batch_destroy(h->b);
+  delete h;
+  return PICP_OK;
+}
+
+extern "C" int picp_set_camera(picp_t* h, int rows, int cols, const float K[9]) {
+  CHECK_ARG(h && K, "picp_set_camera: null argument");
+  CHECK_ARG(rows > 0 && cols > 0, "picp_set_camera: rows/cols must be positive");
+  h->b->rows = rows;
+  h->b->cols = cols;
+  memcpy(h->b->K, K, sizeof(h->b->K));
+  h->b->probs_dirty = true;
+  return PICP_OK;
+}
+
+static int grow(void** ptr, int64_t* cap, int64_t need, size_t elem) {
+  if (need <= *cap) return PICP_OK;
+  if (*ptr) hipFree(*ptr);
+  *ptr = nullptr;
+  const int64_t c = std::max<int64_t>(need, 256);
+  hipError_t e = hipMalloc(ptr, (size_t)c * elem);
+  if (e != hipSuccess) { *cap = 0; return set_err(PICP_ERR_NOMEM, "hipMalloc(%zu): %s", (size_t)c * elem, hipGetErrorString(e)); }
+  *cap = c;
+  return PICP_OK;
+}
+
+extern "C" int picp_set_points(picp_t* h, const float* world, int64_t n_world, const float* image,
+                               int64_t n_image) {
+  CHECK_ARG(h, "picp_set_points: null handle");
+  CHECK_ARG(n_world >= 0 && n_image >= 0, "picp_set_points: negative size");
+  CHECK_ARG((n_world == 0 || world) && (n_image == 0 || image), "picp_set_points: null array");
+  HIP_TRY(hipSetDevice(h->b->device));
+  int rc = grow((void**)&h->world_d, &h->cap_world, 3 * n_world, sizeof(float));
+  if (rc) return rc;
+  rc = grow((void**)&h->image_d, &h->cap_image, 2 * n_image, sizeof(float));
+  if (rc) return rc;
+  if (n_world) HIP_TRY(hipMemcpyAsync(h->world_d, world, (size_t)n_world * 3 * sizeof(float), hipMemcpyHostToDevice, h->b->stream));
+  if (n_image) HIP_TRY(hipMemcpyAsync(h->image_d, image, (size_t)n_image * 2 * sizeof(float), hipMemcpyHostToDevice, h->b->stream));
+  HIP_TRY(hipStreamSynchronize(h->b->stream));
+  h->n_world = n_world;
+  h->n_image = n_image;
+  h->have_points = true;
+  h->gathered = false;
+  // the cached correspondences stay valid as indices but must be re-checked and re-gathered
+  if (h->m >= 0) {
+    for (int64_t k = 0; k < h->m; ++k) {
+      if (h->pairs_h[2 * k] < 0 || h->pairs_h[2 * k] >= n_image || h->pairs_h[2 * k + 1] < 0 || h->pairs_h[2 * k + 1] >= n_world) {
+        h->m = -1;
+        h->pairs_h.clear();
+        break;
+      }
+    }
+  }
+  return PICP_OK;
+}
+
+// Upload + gather the correspondences into the SoA planes if anything changed.
+static int handle_prepare(picp_handle* h) {
+  if (!h->have_points) return set_err(PICP_ERR_STATE, "points not set (call picp_set_points first)");
+  if (h->m < 0) return set_err(PICP_ERR_STATE, "correspondences not set");
+  if (h->gathered) return PICP_OK;
+  picp_batch* b = h->b;
+  HIP_TRY(hipSetDevice(b->device));
+  if (b->total != h->m) {
+    const int64_t offs[2] = {0, h->m};
+    int rc = batch_layout(b, offs, 1);
+    if (rc) return rc;
+  }
+  if (h->m > 0) {
+    int rc = grow((void**)&h->pairs_d, &h->cap_pairs, h->m, sizeof(int2));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(h->pairs_d, h->pairs_h.data(), (size_t)h->m * sizeof(int2), hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(picp_launch_gather(b->stream, h->world_d, h->image_d, h->pairs_d, h->m, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->plane_off[0]));
+  }
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  h->gathered = true;
+  return PICP_OK;
+}
+
+extern "C" int picp_set_correspondences(picp_t* h, const int32_t* pairs, int64_t m) {
+  CHECK_ARG(h, "picp_set_correspondences: null handle");
+  CHECK_ARG(m >= 0 && (m == 0 || pairs), "picp_set_correspondences: bad array");
+  CHECK_ARG(m <= INT32_MAX, "picp_set_correspondences: too many correspondences");
+  if (h->m == m && (m == 0 || memcmp(h->pairs_h.data(), pairs, (size_t)m * 2 * sizeof(int32_t)) == 0))
+    return PICP_OK;  // same array as last time: keep the gathered planes
+  if (!h->have_points) return set_err(PICP_ERR_STATE, "picp_set_correspondences: points not set");
+  for (int64_t k = 0; k < m; ++k) {
+    const int32_t ii = pairs[2 * k], wi = pairs[2 * k + 1];
+    if (ii < 0 || ii >= h->n_image || wi < 0 || wi >= h->n_world)
+      return set_err(PICP_ERR_RANGE, "correspondence %lld = (%d,%d) out of range (image %lld, world %lld)",
+                     (long long)k, ii, wi, (long long)h->n_image, (long long)h->n_world);
+  }
+  h->pairs_h.assign(pairs, pairs + 2 * m);
+  h->m = m;
+  h->gathered = false;
+  return PICP_OK;
+}
+
+extern "C" int picp_set_pose(picp_t* h, const float T[16]) {
+  CHECK_ARG(h && T, "picp_set_pose: null argument");
+  memcpy(h->pose, T, sizeof(h->pose));
+  return PICP_OK;
+}
+
+extern "C" int picp_get_pose(picp_t* h, float T[16]) {
+  CHECK_ARG(h && T, "picp_get_pose: null argument");
+  memcpy(T, h->pose, sizeof(h->pose));
+  return PICP_OK;
+}
+
+static int handle_upload_pose(picp_handle* h) {
+  picp_batch* b = h->b;
+  pose_to_state(h->pose, b->init_h[0]);
+  HIP_TRY(hipMemcpyAsync(b->init_d, b->init_h.data(), sizeof(PicpState), hipMemcpyHostToDevice, b->stream));
+  return PICP_OK;
+}
+
+extern "C" int picp_one_round(picp_t* h, float threshold, float damping, int min_inliers,
+                              int keep_outliers, picp_stats* stats) {
+  CHECK_ARG(h, "picp_one_round: null handle");
+  int rc = handle_prepare(h);
+  if (rc) return rc;
+  picp_batch* b = h->b;
+  picp_params prm;
+  prm.threshold = threshold;
+  prm.damping = damping;
+  prm.min_inliers = min_inliers;
+  prm.keep_outliers = keep_outliers;
+  prm.max_rounds = 1;
+  prm.conv_eps = -1.0f;  // the caller's loop owns the convergence test
+  HIP_TRY(hipSetDevice(b->device));
+  rc = batch_upload_params(b, &prm);
+  if (rc) return rc;
+  rc = handle_upload_pose(h);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
+  HIP_TRY(picp_launch_round(b->stream, b->nblk, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d, b->blk_d,
+                            b->st_d[1], b->st_d[0], b->part_d[1], b->part_d[0], 0, 0));
+  HIP_TRY(picp_launch_round(b->stream, 1, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d, b->blk_d,
+                            b->st_d[0], b->st_d[1], b->part_d[0], b->part_d[1], 1, 1));
+  b->last_rounds = 1;
+  rc = batch_read_results(b);
+  if (rc) return rc;
+  const PicpState& s = b->result_h[0];
+  if (stats) state_to_stats(s, *stats);
+  if (!s.ok) return PICP_TOO_FEW_INLIERS;
+  state_to_pose(s, h->pose);
+  return PICP_OK;
+}
+
+extern "C" int picp_solve(picp_t* h, const picp_params* prm, picp_stats* stats) {
+  CHECK_ARG(h && prm, "picp_solve: null argument");
+  int rc = handle_prepare(h);
+  if (rc) return rc;
+  picp_batch* b = h->b;
+  HIP_TRY(hipSetDevice(b->device));
+  rc = handle_upload_pose(h);
+  if (rc) return rc;
+  rc = picp_batch_solve(b, prm);
+  if (rc) return rc;
+  const PicpState& s = b->result_h[0];
+  if (stats) state_to_stats(s, *stats);
+  state_to_pose(s, h->pose);
+  return PICP_OK;
+}
+
+extern "C" int picp_linearize(picp_t* h, float threshold, int keep_outliers, double H[36],
+                              double bvec[6], picp_stats* stats) {
+  CHECK_ARG(h && H && bvec, "picp_linearize: null argument");
+  int rc = handle_prepare(h);
+  if (rc) return rc;
+  picp_batch* b = h->b;
+  picp_params prm;
+  picp_params_default(&prm);
+  prm.threshold = threshold;
+  prm.keep_outliers = keep_outliers;
+  prm.max_rounds = 1;
+  prm.conv_eps = -1.0f;
+  HIP_TRY(hipSetDevice(b->device));
+  rc = batch_upload_params(b, &prm);
+  if (rc) return rc;
+  rc = handle_upload_pose(h);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
+  HIP_TRY(picp_launch_round(b->stream, b->nblk, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d, b->blk_d,
+                            b->st_d[1], b->st_d[0], b->part_d[1], b->part_d[0], 0, 0));
+  std::vector<float> part((size_t)b->nblk * PICP_NPART);
+  HIP_TRY(hipMemcpyAsync(part.data(), b->part_d[0], part.size() * sizeof(float), hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  double tot[PICP_NPART] = {0};
+  for (int k = 0; k < b->nblk; ++k)
+    for (int e = 0; e < PICP_NPART; ++e) tot[e] += (double)part[(size_t)k * PICP_NPART + e];
+  int idx = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c) {
+      H[c * 6 + r] = tot[PICP_P_H + idx];
+      H[r * 6 + c] = tot[PICP_P_H + idx];
+      ++idx;
+    }
+  for (int r = 0; r < 6; ++r) bvec[r] = tot[PICP_P_B + r];
+  if (stats) {
+    stats->chi_in = (float)tot[PICP_P_CHI_IN];
+    stats->chi_out = (float)tot[PICP_P_CHI_OUT];
+    stats->n_in = (int32_t)tot[PICP_P_N_IN];
+    stats->n_projected = (int32_t)tot[PICP_P_N_PROJ];
+    stats->ok = 1;
+    stats->rounds = 0;
+    stats->converged = 0;
+    stats->reserved = 0;
+  }
+  return PICP_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// triangulation
+// ------------------------------------------------------------------------------------
+extern "C" int picp_projection_matrix(const float K[9], const float T_cw[16], float P[12]) {
+  CHECK_ARG(K && T_cw && P, "picp_projection_matrix: null argument");
+  // inverse of a rigid transform (Eigen Isometry3f::inverse), then K * [R|t]
+  float Ri[9], ti[3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Ri[j * 3 + i] = T_cw[i * 4 + j];
+  for (int i = 0; i < 3; ++i) {
+    float s = Ri[0 * 3 + i] * T_cw[12 + 0];
+    s = s + Ri[1 * 3 + i] * T_cw[12 + 1];
+    s = s + Ri[2 * 3 + i] * T_cw[12 + 2];
+    ti[i] = -s;
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) {
+      float m0 = (j < 3) ? Ri[j * 3 + 0] : ti[0];
+      float m1 = (j < 3) ? Ri[j * 3 + 1] : ti[1];
+      float m2 = (j < 3) ? Ri[j * 3 + 2] : ti[2];
+      float s = K[0 * 3 + i] * m0;
+      s = s + K[1 * 3 + i] * m1;
+      s = s + K[2 * 3 + i] * m2;
+      P[i * 4 + j] = s;
+    }
+  return PICP_OK;
+}
+
+extern "C" int picp_triangulate(int device, const float P1[12], const float P2[12],
+                                const float* uv1, const float* uv2, int64_t q, float* xyz) {
+  CHECK_ARG(P1 && P2, "picp_triangulate: null projection matrix");
+  CHECK_ARG(q >= 0 && (q == 0 || (uv1 && uv2 && xyz)), "picp_triangulate: bad arrays");
+  if (q == 0) return PICP_OK;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  CHECK_ARG(device >= 0 && device < ndev, "picp_triangulate: no such HIP device");
+  HIP_TRY(hipSetDevice(device));
+  const size_t bytes = 2 * 12 * sizeof(float) + (size_t)q * (2 + 2 + 3) * sizeof(float);
+  char* buf = nullptr;
+  HIP_TRY(hipMalloc(&buf, bytes));
+  float* dP = (float*)buf;
+  float* duv1 = dP + 24;
+  float* duv2 = duv1 + 2 * q;
+  float* dxyz = duv2 + 2 * q;
+  hipError_t e = hipMemcpy(dP, P1, 12 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dP + 12, P2, 12 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(duv1, uv1, (size_t)q * 2 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(duv2, uv2, (size_t)q * 2 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = picp_launch_triangulate(nullptr, dP, dP + 12, (const float2*)duv1, (const float2*)duv2, q, dxyz);
+  if (e == hipSuccess) e = hipMemcpy(xyz, dxyz, (size_t)q * 3 * sizeof(float), hipMemcpyDeviceToHost);
+  hipFree(buf);
+  if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_triangulate: %s", hipGetErrorString(e));
+  return PICP_OK;
+}

@@ -1,0 +1,347 @@
+"""picp_amd -- Python binding of libpicp_amd.so (the MI355X PICP hot path, include/picp_c.h).
+
+Thin ctypes layer used by the tests, bench.py and __graft_entry__; the product itself is the
+C-ABI library and the C++ facade (include/pr/*.h).  There is deliberately no CPU fallback:
+if the native library is missing or no HIP device is present, every compute call raises.
+
+Mirrors the reference interface (llepa/02-VisualOdometry):
+  * PICPSolver  -- pr::PICPSolver (src/picp_solver.h:21-82): init / oneRound /
+                   setKernelThreshold / chiInliers / chiOutliers / numInliers / camera pose,
+                   plus solve() = the exec/icp_test.cpp:88-107 loop fused on the device.
+  * Batch       -- independent frames solved together on one device (the batch split).
+  * triangulate -- Cam::triangulatePoints' DLT (src/cam.cpp:94-140).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpicp_amd.so")
+
+OK = 0
+ERR_ARG = -1
+ERR_DEVICE = -2
+ERR_RANGE = -3
+ERR_STATE = -4
+ERR_NOMEM = -5
+TOO_FEW_INLIERS = 1
+
+K_REF = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)  # src/cam.cpp:11-16
+
+# every symbol include/picp_c.h declares (tests check the library exports all of them)
+EXPORTED = [
+    "picp_params_default", "picp_abi_version", "picp_last_error", "picp_device_count",
+    "picp_create", "picp_destroy", "picp_set_camera", "picp_set_points",
+    "picp_set_correspondences", "picp_set_pose", "picp_get_pose", "picp_one_round",
+    "picp_solve", "picp_linearize", "picp_batch_create", "picp_batch_destroy",
+    "picp_batch_set_data", "picp_batch_set_data_device", "picp_batch_set_poses",
+    "picp_batch_get_poses", "picp_batch_get_stats", "picp_batch_solve",
+    "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_info",
+    "picp_triangulate", "picp_projection_matrix",
+]
+
+
+class PicpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("picp error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("chi_in", ctypes.c_float), ("chi_out", ctypes.c_float),
+                ("n_in", ctypes.c_int32), ("ok", ctypes.c_int32), ("rounds", ctypes.c_int32),
+                ("converged", ctypes.c_int32), ("n_projected", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_float), ("damping", ctypes.c_float),
+                ("min_inliers", ctypes.c_int32), ("keep_outliers", ctypes.c_int32),
+                ("max_rounds", ctypes.c_int32), ("conv_eps", ctypes.c_float)]
+
+
+_lib = None
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-j8", "-C", PKG_ROOT])
+
+
+def lib():
+    """Load libpicp_amd.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PicpError(ERR_STATE, "native library %s missing: run `make -C %s`" % (LIB_PATH, PKG_ROOT))
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, i64, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+    fp = ctypes.POINTER(ctypes.c_float)
+    dp = ctypes.POINTER(ctypes.c_double)
+    sp = ctypes.POINTER(Stats)
+    pp = ctypes.POINTER(Params)
+    sig = {
+        "picp_params_default": ([pp], None),
+        "picp_abi_version": ([], i),
+        "picp_last_error": ([], ctypes.c_char_p),
+        "picp_device_count": ([ctypes.POINTER(i)], i),
+        "picp_create": ([ctypes.POINTER(vp), i, i, i, fp], i),
+        "picp_destroy": ([vp], i),
+        "picp_set_camera": ([vp, i, i, fp], i),
+        "picp_set_points": ([vp, fp, i64, fp, i64], i),
+        "picp_set_correspondences": ([vp, ctypes.POINTER(ctypes.c_int32), i64], i),
+        "picp_set_pose": ([vp, fp], i),
+        "picp_get_pose": ([vp, fp], i),
+        "picp_one_round": ([vp, f, f, i, i, sp], i),
+        "picp_solve": ([vp, pp, sp], i),
+        "picp_linearize": ([vp, f, i, dp, dp, sp], i),
+        "picp_batch_create": ([ctypes.POINTER(vp), i, i, ctypes.POINTER(i64), i, i, fp], i),
+        "picp_batch_destroy": ([vp], i),
+        "picp_batch_set_data": ([vp, fp, fp], i),
+        "picp_batch_set_data_device": ([vp, vp, vp, vp, vp, vp], i),
+        "picp_batch_set_poses": ([vp, fp], i),
+        "picp_batch_get_poses": ([vp, fp], i),
+        "picp_batch_get_stats": ([vp, sp], i),
+        "picp_batch_solve": ([vp, pp], i),
+        "picp_batch_solve_async": ([vp, pp], i),
+        "picp_batch_sync": ([vp], i),
+        "picp_batch_time": ([vp, pp, i, fp, fp], i),
+        "picp_batch_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i)], i),
+        "picp_triangulate": ([i, fp, fp, fp, fp, i64, fp], i),
+        "picp_projection_matrix": ([fp, fp, fp], i),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc, allow=()):
+    if rc != OK and rc not in allow:
+        raise PicpError(rc, lib().picp_last_error().decode(errors="replace"))
+    return rc
+
+
+def _fptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a if shape is None else a.reshape(shape)
+
+
+def pose_to_c(T):
+    """4x4 (row, col) -> column-major float[16] (Eigen::Isometry3f memory)."""
+    return np.ascontiguousarray(np.asarray(T, np.float32).T.reshape(16))
+
+
+def pose_from_c(p16):
+    return np.asarray(p16, np.float32).reshape(4, 4).T.copy()
+
+
+def k_to_c(K):
+    return np.ascontiguousarray(np.asarray(K, np.float32).T.reshape(9))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(lib().picp_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def default_params(**kw):
+    p = Params()
+    lib().picp_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class PICPSolver:
+    """pr::PICPSolver over the C-ABI (src/picp_solver.h:21-82).
+
+    init(camera, world_points, image_points) copies the arrays to the device (the reference
+    keeps raw pointers, src/picp_solver.cpp:21-22).  Correspondences are (image idx, world idx)
+    pairs (src/picp_solver.cpp:65-66)."""
+
+    def __init__(self, device=0, rows=480, cols=640, K=K_REF):
+        self._h = ctypes.c_void_p()
+        self.device = device
+        _check(lib().picp_create(ctypes.byref(self._h), device, rows, cols, _fptr(k_to_c(K))))
+        self._threshold = 1000.0  # src/picp_solver.cpp:14
+        self._damping = 1.0       # src/picp_solver.cpp:11
+        self._min_inliers = 0     # src/picp_solver.cpp:12
+        self._stats = Stats()
+
+    def close(self):
+        if self._h:
+            lib().picp_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- reference surface -------------------------------------------------------------
+    def init(self, T_wc, world_points, image_points, rows=None, cols=None, K=None):
+        if rows is not None:
+            _check(lib().picp_set_camera(self._h, rows, cols, _fptr(k_to_c(K))))
+        w = _f32(world_points, (-1,))
+        im = _f32(image_points, (-1,))
+        _check(lib().picp_set_points(self._h, _fptr(w), w.size // 3, _fptr(im), im.size // 2))
+        self.set_pose(T_wc)
+
+    def kernelThreshold(self):
+        return self._threshold
+
+    def setKernelThreshold(self, t):
+        self._threshold = float(t)
+
+    def chiInliers(self):
+        return self._stats.chi_in
+
+    def chiOutliers(self):
+        return self._stats.chi_out
+
+    def numInliers(self):
+        return self._stats.n_in
+
+    def set_pose(self, T_wc):
+        _check(lib().picp_set_pose(self._h, _fptr(pose_to_c(T_wc))))
+
+    def pose(self):
+        out = np.zeros(16, np.float32)
+        _check(lib().picp_get_pose(self._h, _fptr(out)))
+        return pose_from_c(out)
+
+    def set_correspondences(self, pairs):
+        pr = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        _check(lib().picp_set_correspondences(
+            self._h, pr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), pr.shape[0]))
+
+    def oneRound(self, correspondences, keep_outliers=False):
+        """Returns the reference's bool (False when n_in < min_inliers)."""
+        self.set_correspondences(correspondences)
+        rc = _check(lib().picp_one_round(self._h, self._threshold, self._damping,
+                                         self._min_inliers, int(keep_outliers),
+                                         ctypes.byref(self._stats)), allow=(TOO_FEW_INLIERS,))
+        return rc == OK
+
+    # --- extensions ----------------------------------------------------------------------
+    def solve(self, correspondences, max_rounds=50, conv_eps=1e-5, keep_outliers=False):
+        """exec/icp_test.cpp:88-107 fused on the device.  Returns stats dict."""
+        self.set_correspondences(correspondences)
+        prm = default_params(threshold=self._threshold, damping=self._damping,
+                             min_inliers=self._min_inliers, keep_outliers=int(keep_outliers),
+                             max_rounds=max_rounds, conv_eps=conv_eps)
+        _check(lib().picp_solve(self._h, ctypes.byref(prm), ctypes.byref(self._stats)))
+        return self._stats.as_dict()
+
+    def linearize(self, correspondences, keep_outliers=False):
+        self.set_correspondences(correspondences)
+        H = np.zeros(36, np.float64)
+        b = np.zeros(6, np.float64)
+        st = Stats()
+        _check(lib().picp_linearize(self._h, self._threshold, int(keep_outliers),
+                                    H.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                    b.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                    ctypes.byref(st)))
+        return {"H": H.reshape(6, 6).T.copy(), "b": b, **st.as_dict()}
+
+
+class Batch:
+    """Independent PICP problems (frames) solved together on one device."""
+
+    def __init__(self, sizes, device=0, rows=480, cols=640, K=K_REF):
+        sizes = np.asarray(sizes, np.int64)
+        offs = np.zeros(len(sizes) + 1, np.int64)
+        offs[1:] = np.cumsum(sizes)
+        self.offs = offs
+        self.n = len(sizes)
+        self.device = device
+        self._b = ctypes.c_void_p()
+        _check(lib().picp_batch_create(ctypes.byref(self._b), device, self.n,
+                                       offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                       rows, cols, _fptr(k_to_c(K))))
+
+    def close(self):
+        if self._b:
+            lib().picp_batch_destroy(self._b)
+            self._b = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_data(self, xyz, uv):
+        xyz = _f32(xyz, (-1,))
+        uv = _f32(uv, (-1,))
+        assert xyz.size == 3 * self.offs[-1] and uv.size == 2 * self.offs[-1]
+        _check(lib().picp_batch_set_data(self._b, _fptr(xyz), _fptr(uv)))
+
+    def set_poses(self, Ts):
+        Ts = np.asarray(Ts, np.float32).reshape(self.n, 4, 4)
+        flat = np.ascontiguousarray(np.transpose(Ts, (0, 2, 1)).reshape(-1))
+        _check(lib().picp_batch_set_poses(self._b, _fptr(flat)))
+
+    def poses(self):
+        out = np.zeros(16 * self.n, np.float32)
+        _check(lib().picp_batch_get_poses(self._b, _fptr(out)))
+        return np.transpose(out.reshape(self.n, 4, 4), (0, 2, 1)).copy()
+
+    def stats(self):
+        st = (Stats * self.n)()
+        _check(lib().picp_batch_get_stats(self._b, st))
+        return [s.as_dict() for s in st]
+
+    def solve(self, **params):
+        prm = default_params(**params)
+        _check(lib().picp_batch_solve(self._b, ctypes.byref(prm)))
+
+    def solve_async(self, **params):
+        prm = default_params(**params)
+        _check(lib().picp_batch_solve_async(self._b, ctypes.byref(prm)))
+
+    def sync(self):
+        _check(lib().picp_batch_sync(self._b))
+
+    def time(self, reps, **params):
+        prm = default_params(**params)
+        total = ctypes.c_float(0)
+        kus = (ctypes.c_float * 2)()
+        _check(lib().picp_batch_time(self._b, ctypes.byref(prm), reps, ctypes.byref(total), kus))
+        return total.value, (kus[0], kus[1])
+
+    def info(self):
+        tot = ctypes.c_int64(0)
+        nb = ctypes.c_int(0)
+        _check(lib().picp_batch_info(self._b, ctypes.byref(tot), ctypes.byref(nb)))
+        return {"total_corr": tot.value, "n_blocks": nb.value}
+
+
+def projection_matrix(K, T_cw):
+    P = np.zeros(12, np.float32)
+    _check(lib().picp_projection_matrix(_fptr(k_to_c(K)), _fptr(pose_to_c(T_cw)), _fptr(P)))
+    return P.reshape(3, 4)
+
+
+def triangulate(P1, P2, uv1, uv2, device=0):
+    uv1 = _f32(uv1, (-1, 2))
+    uv2 = _f32(uv2, (-1, 2))
+    out = np.zeros((uv1.shape[0], 3), np.float32)
+    _check(lib().picp_triangulate(device, _fptr(_f32(P1, (12,))), _fptr(_f32(P2, (12,))),
+                                  _fptr(uv1), _fptr(uv2), uv1.shape[0], _fptr(out)))
+    return out

@@ -1,0 +1,51 @@
+"""Reader for tests/golden/vo_data.npz, the re-encoded reference dataset (data/).
+
+Frame k's ground-truth world-in-camera pose is (T_world_robot(gt_pose_k) * mount)^-1 with the
+data/camera.dat mount; correspondences between a frame's measurements and world.dat are taken
+by the simulator's ground-truth association id_real (the reference matches descriptors,
+src/my_utilities.h:70-120; with the noise-free data both give the same pairs whenever the
+descriptor match is correct).
+"""
+import os
+
+import numpy as np
+
+from .synth import MOUNT, planar, rigid_inverse
+
+DEFAULT_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "tests", "golden", "vo_data.npz")
+
+
+class VOData:
+    def __init__(self, path=DEFAULT_PATH):
+        d = np.load(path)  # plain arrays, no pickle
+        self.world_id = d["world_id"]
+        self.world_xyz = d["world_xyz"]
+        self.world_desc = d["world_desc"]
+        self.gt_pose = d["gt_pose"]
+        self.odom_pose = d["odom_pose"]
+        self.meas_frame = d["meas_frame"]
+        self.meas_id = d["meas_id"]
+        self.meas_real = d["meas_real"]
+        self.meas_uv = d["meas_uv"]
+        self.meas_desc = d["meas_desc"]
+        self.K = d["K"]
+        self.rows = int(d["rows"])
+        self.cols = int(d["cols"])
+        self.n_frames = self.gt_pose.shape[0]
+        self._id2row = {int(i): r for r, i in enumerate(self.world_id)}
+
+    def frame(self, k):
+        sel = self.meas_frame == k
+        return {"uv": self.meas_uv[sel], "id_meas": self.meas_id[sel],
+                "id_real": self.meas_real[sel], "desc": self.meas_desc[sel]}
+
+    def T_wc(self, k, pose=None):
+        p = self.gt_pose[k] if pose is None else pose
+        return rigid_inverse(planar(float(p[0]), float(p[1]), float(p[2])) @ MOUNT).astype(np.float32)
+
+    def correspondences(self, k):
+        """(image idx, world idx) pairs of frame k by id_real."""
+        f = self.frame(k)
+        pairs = [(i, self._id2row[int(r)]) for i, r in enumerate(f["id_real"]) if int(r) in self._id2row]
+        return np.array(pairs, np.int32).reshape(-1, 2)

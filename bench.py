@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""PICP hot-path benchmark (BASELINE.json metric: PICP iterations/sec @ N correspondences).
+
+Default workload (N=1): BASELINE configs[1] = C2, a single synthetic frame with 100,000
+3D<->2D correspondences, 50 Gauss-Newton rounds (convergence test disabled for timing), on one
+MI355X.  One "step" = one full 50-round solve of the frame (inputs resident in HBM, one hipGraph
+replay: initial-state copy + 50 linearize launches + 1 finalize launch).  value = rounds
+executed by all ranks / max-over-ranks wall time of the timed region.
+
+Multi-GPU (torchrun, one process per GPU): every rank solves its own independent frame
+(seed 42 + rank) -> weak scaling, no data-path collective; rank 0 gathers the final poses once
+after timing (RCCL all_gather) to check them.
+
+Printed JSON also carries:
+  roofline     : dominant kernel = picp_round_kernel (linearize launch); achieved = 20 algorithmic
+                 bytes per correspondence (x,y,z,u,v float32 SoA) x N / mean launch duration,
+                 the launch duration measured with HIP event pairs on the library's stream.
+  cpu_baseline : the oracle's faithful float32 single-thread restatement (kind "port"), timed on
+                 this host on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "02-visualodometry_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+BYTES_PER_CORR = 20    # x,y,z,u,v float32 per correspondence-round
+
+WORKLOADS = {
+    "c2": dict(n=100000, problems=1, outlier=0.0, desc="C2 single-frame PICP, 100k synthetic correspondences, 50 GN rounds"),
+    "c3": dict(n=1000000, problems=1, outlier=0.3, desc="C3 single-frame PICP, 1M synthetic correspondences, 30% outliers + chi2 rejection, 50 GN rounds"),
+    "c4": dict(n=10000, problems=128, outlier=0.0, desc="C4 batch of independent frames x 10k correspondences (128 per GPU), 50 GN rounds each"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--rounds", type=int, default=50)
+    ap.add_argument("--n", type=int, default=0, help="override correspondences per frame")
+    ap.add_argument("--problems", type=int, default=0, help="override frames per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch  # plumbing only: process group, barrier, device sync (loaded before the HIP lib)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import picp_amd
+    from picp_amd import synth
+
+    wl = dict(WORKLOADS[args.workload])
+    n = args.n or wl["n"]
+    nprob = args.problems or wl["problems"]
+    R = args.rounds
+    thr = 3000.0
+
+    # ---- inputs (seeded, resident on the device before timing) ----
+    if nprob == 1:
+        p = synth.make_problem(n, seed=42 + rank, outlier_frac=wl["outlier"], pixel_noise=0.5, shuffle=False)
+        xyz, uv, T_init, T_gt = p["xyz"], p["uv"], p["T_init"][None], p["T_gt"][None]
+        sizes = [n]
+    else:
+        bt = synth.make_batch(nprob, n, base_seed=1000, first=rank * nprob,
+                              outlier_frac=wl["outlier"], pixel_noise=0.5)
+        xyz, uv, T_init, T_gt, sizes = bt["xyz"], bt["uv"], bt["T_init"], bt["T_gt"], bt["sizes"]
+    b = picp_amd.Batch(sizes, device=local if world > 1 else 0)
+    b.set_data(xyz, uv)
+    b.set_poses(T_init)
+    params = dict(threshold=thr, max_rounds=R, conv_eps=-1.0)
+
+    def sync_all():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        b.solve_async(**params)
+    b.sync()
+    sync_all()
+
+    barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.solve_async(**params)
+    b.sync()
+    sync_all()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- correctness of what was timed (outside the timed region) ----
+    poses = b.poses()
+    err = max(synth.se3_log_norm(poses[i], T_gt[i]) for i in range(len(sizes)))
+    if dist is not None:
+        mine = torch.tensor(poses.reshape(-1), device="cuda")
+        allp = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allp, mine)  # RCCL over xGMI: the only collective of the batch split
+        errs = torch.tensor([err], dtype=torch.float64, device="cuda")
+        dist.all_reduce(errs, op=dist.ReduceOp.MAX)
+        err = float(errs.item())
+
+    # ---- per-launch kernel duration (HIP event pairs on the library's stream) ----
+    total_ms, (lin_us, fin_us) = b.time(3, **params)
+    info = b.info()
+    corr_per_launch = int(info["total_corr"])
+    achieved = BYTES_PER_CORR * corr_per_launch / (lin_us * 1e-6) / 1e9 if lin_us > 0 else 0.0
+
+    rounds_total = world * len(sizes) * R * args.steps
+    value = rounds_total / elapsed
+    out = {
+        "metric": "PICP iterations/sec @ %d correspondences" % n,
+        "value": round(value, 2),
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded generator of SURVEY.md §8d; inputs resident in HBM)",
+        "config": {
+            "workload": wl["desc"],
+            "n_corr": n,
+            "frames_per_gpu": len(sizes),
+            "rounds": R,
+            "threshold": thr,
+            "convergence_test": "disabled for timing",
+            "parallelism": "independent frames, one process per GPU" if world > 1 else "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None,
+            "kernel": "picp_round_kernel (linearize launch)",
+            "kernel_us": round(lin_us, 3),
+            "finalize_us": round(fin_us, 3),
+            "bytes_per_launch": BYTES_PER_CORR * corr_per_launch,
+            "blocks_per_launch": info["n_blocks"],
+        },
+        "pose_err_vs_gt_se3": err,
+    }
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(xyz[: sizes[0]], uv[: sizes[0]], T_init[0], R, thr, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(xyz, uv, T_init, R, thr, budget_s):
+    """Oracle (faithful float32, sequential) single thread on one frame of the workload:
+    whole R-round solves until the time budget is used (at least one)."""
+    import platform
+
+    import numpy as np
+    import oracle as O
+    x, y, z = (np.ascontiguousarray(xyz[:, i]) for i in range(3))
+    u, v = np.ascontiguousarray(uv[:, 0]), np.ascontiguousarray(uv[:, 1])
+    K = O._k9  # noqa: F841  (ensure module import)
+    Kref = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
+    solves, t0 = 0, time.perf_counter()
+    while True:
+        O.solve_soa(T_init, Kref, 480, 640, x, y, z, u, v, thr, mode=O.MODE_FAITHFUL,
+                    max_rounds=R, conv_eps=-1.0)
+        solves += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(solves * R / el, 3), "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, "
+                      "gcc -O2, 1 thread) in %.1f s on %s" % (solves, R, len(x), el, model)}
+
+
+if __name__ == "__main__":
+    main()

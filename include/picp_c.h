@@ -1,0 +1,159 @@
+/*
+ * picp_c.h -- C-ABI of libpicp_amd.so, the MI355X (gfx950) PICP hot path.
+ *
+ * This is the drop-in boundary for the reference's pr::PICPSolver / pr::Camera
+ * (llepa/02-VisualOdometry; paths below are relative to the reference repo root).  Plain
+ * pointers and sizes only; no C++ or framework types.  Every call returns an int status
+ * (PICP_OK == 0); nothing throws across the ABI.  picp_last_error() returns a
+ * thread-local description of the last failure.
+ *
+ * Memory layouts (identical to the reference's Eigen types):
+ *   pose  T_wc[16] : 4x4 float COLUMN-major (Eigen::Isometry3f), the world-in-camera pose
+ *                    (pr::Camera::worldInCameraPose, src/camera.h:51).
+ *   K[9]           : 3x3 float column-major (Eigen::Matrix3f, src/camera.h:45).
+ *   world xyz      : float[3*n] packed (Vector3fVector, src/defs.h:22).
+ *   image uv       : float[2*n] packed (Vector2fVector, src/defs.h:23).
+ *   pairs          : int32[2*m] (first = image index, second = world index)
+ *                    (IntPairVector, src/defs.h:209-211; src/picp_solver.cpp:65-66).
+ *   P[12]          : 3x4 float ROW-major projection matrix (cv::Mat, src/cam.cpp:111-112).
+ *
+ * Threading: a handle is bound to one HIP device and owns one HIP stream; a handle must
+ * not be used from two threads at once (the reference solver is single-threaded too).
+ */
+#ifndef PICP_C_H
+#define PICP_C_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PICP_ABI_VERSION 1
+
+/* status codes */
+#define PICP_OK 0
+#define PICP_ERR_ARG -1      /* null pointer / bad size / bad parameter           */
+#define PICP_ERR_DEVICE -2   /* HIP runtime error (see picp_last_error)           */
+#define PICP_ERR_RANGE -3    /* a correspondence index is out of range            */
+#define PICP_ERR_STATE -4    /* call order violated (e.g. round before set_points)*/
+#define PICP_ERR_NOMEM -5    /* device allocation failed                          */
+#define PICP_TOO_FEW_INLIERS 1 /* oneRound returned false: n_in < min_inliers
+                                  (src/picp_solver.cpp:97-100); pose not updated   */
+
+typedef struct picp_handle picp_t;
+typedef struct picp_batch picp_batch_t;
+
+/* Solver statistics, the reference's accessors plus the icp_test loop outcome. */
+typedef struct picp_stats {
+  float chi_in;       /* PICPSolver::chiInliers  (src/picp_solver.h:47)  */
+  float chi_out;      /* PICPSolver::chiOutliers (src/picp_solver.h:50)  */
+  int32_t n_in;       /* PICPSolver::numInliers  (src/picp_solver.h:53)  */
+  int32_t ok;         /* return value of the last oneRound               */
+  int32_t rounds;     /* oneRound calls executed                          */
+  int32_t converged;  /* exec/icp_test.cpp:92 convergenceReached          */
+  int32_t n_projected;/* correspondences that passed projectPoint         */
+  int32_t reserved;
+} picp_stats;
+
+/* Solver parameters. picp_params_default() gives the reference's values. */
+typedef struct picp_params {
+  float threshold;      /* kernel threshold; PICPSolver ctor default 1000 (src/picp_solver.cpp:14),
+                           icp_test uses 3000 (exec/icp_test.cpp:86)                          */
+  float damping;        /* 1 (src/picp_solver.cpp:11)                                          */
+  int32_t min_inliers;  /* 0 (src/picp_solver.cpp:12)                                          */
+  int32_t keep_outliers;/* 0 in icp_test (exec/icp_test.cpp:95)                                */
+  int32_t max_rounds;   /* 50 (exec/icp_test.cpp:88)                                           */
+  float conv_eps;       /* 1e-5 relative chi_in change (exec/icp_test.cpp:91); < 0 disables   */
+} picp_params;
+
+void picp_params_default(picp_params* p);
+int picp_abi_version(void);
+const char* picp_last_error(void);
+int picp_device_count(int* n);
+
+/* ---------------- single-problem handle: the pr::PICPSolver drop-in ---------------- */
+
+/* Replaces PICPSolver() + the Camera passed to init (src/picp_solver.cpp:8-15,17-20). */
+int picp_create(picp_t** out, int device, int rows, int cols, const float K[9]);
+int picp_destroy(picp_t* h);
+int picp_set_camera(picp_t* h, int rows, int cols, const float K[9]);
+
+/* Replaces PICPSolver::init's world/image arguments (src/picp_solver.cpp:17-23).  The
+ * arrays are COPIED to device memory (the reference stores raw pointers; its icp_test
+ * passes temporaries, exec/icp_test.cpp:81-85). */
+int picp_set_points(picp_t* h, const float* world_xyz, int64_t n_world,
+                    const float* image_uv, int64_t n_image);
+
+/* Correspondences for the following rounds (the argument of PICPSolver::oneRound,
+ * src/picp_solver.h:59).  Indices are range-checked (PICP_ERR_RANGE); an identical
+ * repeated array is detected and not re-uploaded. */
+int picp_set_correspondences(picp_t* h, const int32_t* pairs, int64_t m);
+
+/* Camera::setWorldInCameraPose / worldInCameraPose (src/camera.h:51-52) */
+int picp_set_pose(picp_t* h, const float T_wc[16]);
+int picp_get_pose(picp_t* h, float T_wc[16]);
+
+/* PICPSolver::oneRound (src/picp_solver.cpp:93-105): linearize + damping + min-inlier
+ * check + LDLT solve + left update.  Returns PICP_OK, or PICP_TOO_FEW_INLIERS when the
+ * reference returns false.  stats may be NULL. */
+int picp_one_round(picp_t* h, float threshold, float damping, int min_inliers,
+                   int keep_outliers, picp_stats* stats);
+
+/* The whole exec/icp_test.cpp:88-107 loop fused on the device (one graph launch, no host
+ * round trip per round). */
+int picp_solve(picp_t* h, const picp_params* params, picp_stats* stats);
+
+/* Linearize at the current pose without updating it (H 6x6 column-major, b 6), for
+ * parity testing against PICPSolver::linearize (src/picp_solver.cpp:56-91). */
+int picp_linearize(picp_t* h, float threshold, int keep_outliers, double H[36], double b[6],
+                   picp_stats* stats);
+
+/* ---------------- batched independent problems (frames) on one device ---------------- */
+
+/* corr_offsets[n_problems+1]: problem i owns correspondences [off[i], off[i+1]) of the
+ * arrays given to picp_batch_set_data.  Camera shared by all problems. */
+int picp_batch_create(picp_batch_t** out, int device, int n_problems,
+                      const int64_t* corr_offsets, int rows, int cols, const float K[9]);
+int picp_batch_destroy(picp_batch_t* b);
+
+/* Matched correspondences, already gathered: xyz[3*total] world points and uv[2*total]
+ * image points (pairs (i,i)); copied to the device SoA planes. */
+int picp_batch_set_data(picp_batch_t* b, const float* xyz, const float* uv);
+/* Device-resident variant: the five SoA planes of length total, already on this device
+ * (e.g. produced by a previous kernel); copied device-to-device. */
+int picp_batch_set_data_device(picp_batch_t* b, const float* d_x, const float* d_y,
+                               const float* d_z, const float* d_u, const float* d_v);
+
+int picp_batch_set_poses(picp_batch_t* b, const float* T_wc /* 16*n_problems */);
+int picp_batch_get_poses(picp_batch_t* b, float* T_wc /* 16*n_problems */);
+int picp_batch_get_stats(picp_batch_t* b, picp_stats* stats /* n_problems */);
+
+/* Fused icp_test loop for every problem; blocking. */
+int picp_batch_solve(picp_batch_t* b, const picp_params* params);
+/* Same, enqueued on the batch's stream (graph replay); pair with picp_batch_sync. */
+int picp_batch_solve_async(picp_batch_t* b, const picp_params* params);
+int picp_batch_sync(picp_batch_t* b);
+
+/* Time `reps` back-to-back fused solves on the batch's stream with HIP events.
+ * total_ms = elapsed of the whole region; kernel_us[0] = mean duration of one linearize
+ * round launch (event pairs around each round kernel, separate instrumented pass),
+ * kernel_us[1] = mean duration of the finalize launch. */
+int picp_batch_time(picp_batch_t* b, const picp_params* params, int reps, float* total_ms,
+                    float kernel_us[2]);
+/* Number of linearize blocks per launch and total correspondences (introspection). */
+int picp_batch_info(picp_batch_t* b, int64_t* total_corr, int* n_blocks);
+
+/* ---------------- linear triangulation (cv::triangulatePoints replacement) ---------------- */
+
+/* src/cam.cpp:94-140: per point DLT with two 3x4 row-major projection matrices, then
+ * dehomogenisation.  uv1/uv2: float[2*q]; xyz_out: float[3*q].  Host pointers. */
+int picp_triangulate(int device, const float P1[12], const float P2[12], const float* uv1,
+                     const float* uv2, int64_t q, float* xyz_out);
+/* Helper: P = K * inverse(T_cw)(0:3,0:4) from a camera-in-world pose (src/cam.cpp:109-112). */
+int picp_projection_matrix(const float K[9], const float T_cw[16], float P[12]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PICP_C_H */

@@ -1,0 +1,199 @@
+"""ctypes binding of the CPU oracle (oracle/picp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, and only as the checker / the timed CPU baseline.  The product path in
+02-visualodometry_amd/ never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libpicp_oracle.so")
+
+MODE_FAITHFUL = 0
+MODE_F64 = 1
+
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+
+
+class Lin(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_double * 36), ("b", ctypes.c_double * 6),
+                ("chi_in", ctypes.c_double), ("chi_out", ctypes.c_double),
+                ("n_in", ctypes.c_int32), ("n_projected", ctypes.c_int32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("chi_in", ctypes.c_float), ("chi_out", ctypes.c_float),
+                ("n_in", ctypes.c_int32), ("ok", ctypes.c_int32)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        i, i64, f = ctypes.c_int, ctypes.c_int64, ctypes.c_float
+        L.or_project_point.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p]
+        L.or_project_point.restype = i
+        L.or_error_and_jacobian.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _f32p, _f32p]
+        L.or_error_and_jacobian.restype = i
+        L.or_linearize.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _i32p, i64, f, i, i,
+                                   ctypes.POINTER(Lin)]
+        L.or_linearize_soa.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                       i64, f, i, i, ctypes.POINTER(Lin)]
+        L.or_v2t_euler.argtypes = [_f32p, _f32p]
+        L.or_ldlt_solve6_f.argtypes = [_f32p, _f32p, _f32p]
+        L.or_ldlt_solve6_d.argtypes = [_f64p, _f64p, _f64p]
+        L.or_one_round.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _i32p, i64, f, f, i, i, i,
+                                   ctypes.POINTER(Stats)]
+        L.or_one_round.restype = i
+        L.or_solve.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _i32p, i64, f, f, i, i, i, i,
+                               f, ctypes.POINTER(Stats), ctypes.POINTER(ctypes.c_int)]
+        L.or_solve.restype = i
+        L.or_solve_soa.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _f32p, _f32p, _f32p, i64,
+                                   f, f, i, i, i, i, f, ctypes.POINTER(Stats),
+                                   ctypes.POINTER(ctypes.c_int)]
+        L.or_solve_soa.restype = i
+        L.or_triangulate.argtypes = [_f32p, _f32p, _f32p, _f32p, i64, _f32p]
+        L.or_projection_matrix.argtypes = [_f32p, _f32p, _f32p]
+        L.or_iso_inverse.argtypes = [_f32p, _f32p]
+        _lib = L
+    return _lib
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _pose16(T):
+    """4x4 numpy (row, col) -> column-major float[16] (Eigen Isometry3f memory)."""
+    return _f32(np.asarray(T, dtype=np.float32).T.reshape(16))
+
+
+def _pose44(p16):
+    return np.asarray(p16, dtype=np.float32).reshape(4, 4).T.copy()
+
+
+def _k9(K):
+    return _f32(np.asarray(K, dtype=np.float32).T.reshape(9))
+
+
+def project_point(T, K, rows, cols, p):
+    out = np.zeros(2, np.float32)
+    ok = lib().or_project_point(_pose16(T), _k9(K), rows, cols, _f32(p), out)
+    return bool(ok), out
+
+
+def error_and_jacobian(T, K, rows, cols, p, z):
+    e = np.zeros(2, np.float32)
+    J = np.zeros(12, np.float32)
+    ok = lib().or_error_and_jacobian(_pose16(T), _k9(K), rows, cols, _f32(p), _f32(z), e, J)
+    return bool(ok), e, J.reshape(6, 2).T.copy()
+
+
+def _lin_dict(lin):
+    return {"H": np.array(lin.H, np.float64).reshape(6, 6).T.copy(),
+            "b": np.array(lin.b, np.float64), "chi_in": lin.chi_in, "chi_out": lin.chi_out,
+            "n_in": lin.n_in, "n_projected": lin.n_projected}
+
+
+def linearize(T, K, rows, cols, world, image, pairs, threshold, keep_outliers=False,
+              mode=MODE_F64):
+    lin = Lin()
+    pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+    lib().or_linearize(_pose16(T), _k9(K), rows, cols, _f32(world).reshape(-1),
+                       _f32(image).reshape(-1), pairs.reshape(-1), pairs.shape[0],
+                       threshold, int(keep_outliers), mode, ctypes.byref(lin))
+    return _lin_dict(lin)
+
+
+def linearize_soa(T, K, rows, cols, x, y, z, u, v, threshold, keep_outliers=False,
+                  mode=MODE_F64):
+    lin = Lin()
+    lib().or_linearize_soa(_pose16(T), _k9(K), rows, cols, _f32(x), _f32(y), _f32(z),
+                           _f32(u), _f32(v), len(x), threshold, int(keep_outliers), mode,
+                           ctypes.byref(lin))
+    return _lin_dict(lin)
+
+
+def v2t_euler(v):
+    T = np.zeros(16, np.float32)
+    lib().or_v2t_euler(_f32(v), T)
+    return _pose44(T)
+
+
+def one_round(T, K, rows, cols, world, image, pairs, threshold, damping=1.0, min_inliers=0,
+              keep_outliers=False, mode=MODE_FAITHFUL):
+    p = _pose16(T)
+    st = Stats()
+    pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+    ok = lib().or_one_round(p, _k9(K), rows, cols, _f32(world).reshape(-1),
+                            _f32(image).reshape(-1), pairs.reshape(-1), pairs.shape[0],
+                            threshold, damping, min_inliers, int(keep_outliers), mode,
+                            ctypes.byref(st))
+    return bool(ok), _pose44(p), {"chi_in": st.chi_in, "chi_out": st.chi_out, "n_in": st.n_in}
+
+
+def solve(T, K, rows, cols, world, image, pairs, threshold, damping=1.0, min_inliers=0,
+          keep_outliers=False, mode=MODE_F64, max_rounds=50, conv_eps=1e-5):
+    p = _pose16(T)
+    st = Stats()
+    conv = ctypes.c_int(0)
+    pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+    rounds = lib().or_solve(p, _k9(K), rows, cols, _f32(world).reshape(-1),
+                            _f32(image).reshape(-1), pairs.reshape(-1), pairs.shape[0],
+                            threshold, damping, min_inliers, int(keep_outliers), mode,
+                            max_rounds, conv_eps, ctypes.byref(st), ctypes.byref(conv))
+    return _pose44(p), {"chi_in": st.chi_in, "chi_out": st.chi_out, "n_in": st.n_in,
+                        "ok": st.ok, "rounds": rounds, "converged": bool(conv.value)}
+
+
+def solve_soa(T, K, rows, cols, x, y, z, u, v, threshold, damping=1.0, min_inliers=0,
+              keep_outliers=False, mode=MODE_F64, max_rounds=50, conv_eps=1e-5):
+    p = _pose16(T)
+    st = Stats()
+    conv = ctypes.c_int(0)
+    rounds = lib().or_solve_soa(p, _k9(K), rows, cols, _f32(x), _f32(y), _f32(z), _f32(u),
+                                _f32(v), len(x), threshold, damping, min_inliers,
+                                int(keep_outliers), mode, max_rounds, conv_eps,
+                                ctypes.byref(st), ctypes.byref(conv))
+    return _pose44(p), {"chi_in": st.chi_in, "chi_out": st.chi_out, "n_in": st.n_in,
+                        "ok": st.ok, "rounds": rounds, "converged": bool(conv.value)}
+
+
+def ldlt_solve6(A, rhs, double=True):
+    x = np.zeros(6, np.float64 if double else np.float32)
+    if double:
+        lib().or_ldlt_solve6_d(np.ascontiguousarray(np.asarray(A, np.float64).T.reshape(36)),
+                               np.ascontiguousarray(rhs, np.float64), x)
+    else:
+        lib().or_ldlt_solve6_f(_f32(np.asarray(A, np.float32).T.reshape(36)), _f32(rhs), x)
+    return x
+
+
+def projection_matrix(K, T_cw):
+    P = np.zeros(12, np.float32)
+    lib().or_projection_matrix(_k9(K), _pose16(T_cw), P)
+    return P.reshape(3, 4)
+
+
+def triangulate(P1, P2, uv1, uv2):
+    uv1 = _f32(uv1).reshape(-1, 2)
+    uv2 = _f32(uv2).reshape(-1, 2)
+    out = np.zeros((uv1.shape[0], 3), np.float32)
+    lib().or_triangulate(_f32(P1).reshape(12), _f32(P2).reshape(12), uv1.reshape(-1),
+                         uv2.reshape(-1), uv1.shape[0], out.reshape(-1))
+    return out

@@ -1,0 +1,115 @@
+/*
+ * picp_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference PICP hot path (llepa/02-VisualOdometry) used as the
+ * parity checker for the MI355X implementation.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library; the product path
+ * (02-visualodometry_amd/) never links or calls it.
+ *
+ * The reference itself cannot be compiled here (it needs Eigen3 + OpenCV, neither is
+ * installed), so this is a restatement, pinned by the known-answer tests
+ * built from the reference's own noise-free data/ (tests/golden/).
+ *
+ * Conventions (identical to the C-ABI in include/picp_c.h):
+ *   pose  T[16]  : 4x4 float, COLUMN-major (Eigen::Isometry3f memory layout),
+ *                  T(i,j) = T[j*4+i]; this is the world-in-camera pose.
+ *   K[9]         : 3x3 float, column-major (Eigen::Matrix3f layout).
+ *   world[3*W]   : packed xyz (Vector3fVector layout, src/defs.h:22).
+ *   image[2*I]   : packed uv  (Vector2fVector layout, src/defs.h:23).
+ *   pairs[2*M]   : int32 (first = image index, second = world index) (IntPairVector,
+ *                  src/defs.h:209-211, src/picp_solver.cpp:65-66).
+ *   H[36]        : 6x6 column-major, both triangles.
+ */
+#ifndef PICP_ORACLE_H
+#define PICP_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* accumulation modes of or_linearize */
+#define OR_MODE_FAITHFUL 0 /* float32 sequential accumulation, float LDLT (the reference's own arithmetic) */
+#define OR_MODE_F64      1 /* per-correspondence float32 math, float64 accumulation + float64 LDLT */
+
+typedef struct {
+  double H[36];
+  double b[6];
+  double chi_in;
+  double chi_out;
+  int32_t n_in;
+  int32_t n_projected; /* correspondences that passed projectPoint (not in the reference API) */
+} or_lin_t;
+
+typedef struct {
+  float chi_in;
+  float chi_out;
+  int32_t n_in;
+  int32_t ok; /* oneRound's return value */
+} or_stats_t;
+
+/* src/camera.h:24-36 */
+int or_project_point(const float T[16], const float K[9], int rows, int cols,
+                     const float p[3], float img[2]);
+
+/* src/picp_solver.cpp:26-54 ; J is 2x6 column-major (J(r,c) = J[c*2+r]) */
+int or_error_and_jacobian(const float T[16], const float K[9], int rows, int cols,
+                          const float p[3], const float z[2], float e[2], float J[12]);
+
+/* src/picp_solver.cpp:56-91 */
+void or_linearize(const float T[16], const float K[9], int rows, int cols,
+                  const float* world, const float* image, const int32_t* pairs, int64_t m,
+                  float threshold, int keep_outliers, int mode, or_lin_t* out);
+
+/* Same as or_linearize but over already-gathered SoA arrays (x,y,z,u,v), i.e. pairs (i,i).
+ * Used for the large synthetic configurations where the gather is the identity. */
+void or_linearize_soa(const float T[16], const float K[9], int rows, int cols,
+                      const float* x, const float* y, const float* z, const float* u,
+                      const float* v, int64_t m, float threshold, int keep_outliers, int mode,
+                      or_lin_t* out);
+
+/* src/defs.h:100-136 */
+void or_v2t_euler(const float v[6], float T[16]);
+
+/* Eigen LDLT (diagonal pivoting) restatement, as used by src/picp_solver.cpp:102 */
+void or_ldlt_solve6_f(const float A[36], const float rhs[6], float x[6]);
+void or_ldlt_solve6_d(const double A[36], const double rhs[6], double x[6]);
+
+/* src/picp_solver.cpp:93-105 ; updates T in place. returns oneRound's bool. */
+int or_one_round(float T[16], const float K[9], int rows, int cols, const float* world,
+                 const float* image, const int32_t* pairs, int64_t m, float threshold,
+                 float damping, int min_inliers, int keep_outliers, int mode,
+                 or_stats_t* stats);
+
+/* The driver loop of exec/icp_test.cpp:88-107 (max_rounds, relative-chi convergence).
+ * soa != 0 => world=(x,y,z) planes and image=(u,v) planes with pairs ignored (identity).
+ * Returns rounds executed (oneRound calls); *converged set as icp_test's flag. */
+int or_solve(float T[16], const float K[9], int rows, int cols, const float* world,
+             const float* image, const int32_t* pairs, int64_t m, float threshold,
+             float damping, int min_inliers, int keep_outliers, int mode, int max_rounds,
+             float conv_eps, or_stats_t* last_stats, int* converged);
+
+/* Same loop over SoA planes (x,y,z,u,v). */
+int or_solve_soa(float T[16], const float K[9], int rows, int cols, const float* x,
+                 const float* y, const float* z, const float* u, const float* v, int64_t m,
+                 float threshold, float damping, int min_inliers, int keep_outliers, int mode,
+                 int max_rounds, float conv_eps, or_stats_t* last_stats, int* converged);
+
+/* Linear (DLT) triangulation, OpenCV cv::triangulatePoints + convertPointsFromHomogeneous
+ * as called from src/cam.cpp:115-118.  P1,P2 are 3x4 ROW-major (cv::Mat layout).
+ * uv1/uv2 packed float2, xyz_out packed float3.  Smallest right singular vector via a
+ * cyclic Jacobi eigen-decomposition of A^T A in long double (independent of the GPU's
+ * one-sided Jacobi SVD). */
+void or_triangulate(const float P1[12], const float P2[12], const float* uv1, const float* uv2,
+                    int64_t q, float* xyz_out);
+
+/* P = K * inverse(T_camera_in_world)(0:3,0:4) as src/cam.cpp:109-112 (row-major out) */
+void or_projection_matrix(const float K[9], const float T_cw[16], float P[12]);
+
+/* Eigen::Isometry3f::inverse() (rigid inverse) */
+void or_iso_inverse(const float T[16], float Tinv[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

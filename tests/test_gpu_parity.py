@@ -1,0 +1,307 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances (BASELINE.json north_star: poses within 1e-4 on SE(3) log):
+  * pose after a solve      : se3_log_norm(gpu, oracle_f64) < 1e-4
+  * inlier/outlier/skip gate: n_in and n_projected EXACT at the same pose (the gate is
+                              evaluated with the oracle's exact float operation order)
+  * H, b, chi               : relative 1e-5 of the largest entry (float32 per-thread partial
+                              sums + double cross-block reduction vs the oracle's float64
+                              sequential sum)
+  * triangulation           : 1e-5 relative (double DLT on both sides, different SVD methods)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4
+THR = 3000.0  # exec/icp_test.cpp:86
+
+
+def _synth():
+    from picp_amd import synth
+    return synth
+
+
+def _lin_close(got, ref, rtol=1e-5):
+    sH = np.abs(ref["H"]).max()
+    np.testing.assert_allclose(got["H"], ref["H"], rtol=rtol, atol=rtol * sH)
+    sb = max(np.abs(ref["b"]).max(), 1e-30)
+    np.testing.assert_allclose(got["b"], ref["b"], rtol=rtol, atol=rtol * sb)
+    np.testing.assert_allclose(got["chi_in"], ref["chi_in"], rtol=rtol, atol=1e-6)
+    np.testing.assert_allclose(got["chi_out"], ref["chi_out"], rtol=rtol, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,seed,of,noise", [(1, 0, 0.0, 0.0), (17, 1, 0.0, 0.0), (1000, 0, 0.0, 0.0),
+                                             (1000, 1, 0.3, 0.5), (20000, 2, 0.0, 0.5),
+                                             (20000, 3, 0.3, 0.5), (100003, 4, 0.3, 0.5)])
+@pytest.mark.parametrize("keep", [0, 1])
+def test_linearize_matches_oracle(native, oracle, n, seed, of, noise, keep):
+    synth = _synth()
+    p = synth.make_problem(n, seed=seed, outlier_frac=of, pixel_noise=noise)
+    s = native.PICPSolver(rows=480, cols=640, K=p["K"])
+    s.init(p["T_init"], p["world"], p["image"])
+    s.setKernelThreshold(THR)
+    got = s.linearize(p["pairs"], keep_outliers=bool(keep))
+    ref = oracle.linearize(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"], THR,
+                           keep_outliers=keep, mode=oracle.MODE_F64)
+    assert got["n_in"] == ref["n_in"]
+    assert got["n_projected"] == ref["n_projected"]
+    _lin_close(got, ref)
+
+
+def test_linearize_matches_golden_vectors(native):
+    synth = _synth()
+    g = np.load(os.path.join(GOLDEN, "picp_golden.npz"))
+    for name in ("s0_n1k", "s1_n1k_out30"):
+        s = native.PICPSolver()
+        s.init(g[name + "/T_init"], g[name + "/world"], g[name + "/image"])
+        s.setKernelThreshold(THR)
+        for keep in (0, 1):
+            got = s.linearize(g[name + "/pairs"], keep_outliers=bool(keep))
+            tag = "%s/lin_keep%d" % (name, keep)
+            sc = g[tag + "/scal"]
+            ref = {"H": g[tag + "/H"], "b": g[tag + "/b"], "chi_in": sc[0], "chi_out": sc[1]}
+            assert got["n_in"] == int(sc[2]) and got["n_projected"] == int(sc[3])
+            _lin_close(got, ref)
+        st = s.solve(g[name + "/pairs"], max_rounds=50, conv_eps=-1.0)
+        assert synth.se3_log_norm(s.pose(), g[name + "/solve_f64/T"]) < POSE_TOL
+        assert st["rounds"] == 50
+
+
+def test_one_round_matches_oracle(native, oracle):
+    synth = _synth()
+    p = synth.make_problem(5000, seed=7, outlier_frac=0.2, pixel_noise=0.5)
+    s = native.PICPSolver()
+    s.init(p["T_init"], p["world"], p["image"])
+    s.setKernelThreshold(THR)
+    T = p["T_init"].copy()
+    for r in range(5):
+        ok = s.oneRound(p["pairs"], False)
+        okr, T, st = oracle.one_round(T, p["K"], 480, 640, p["world"], p["image"], p["pairs"], THR,
+                                      mode=oracle.MODE_F64)
+        assert ok and okr
+        assert s.numInliers() == st["n_in"]
+        np.testing.assert_allclose(s.chiInliers(), st["chi_in"], rtol=1e-5)
+        assert synth.se3_log_norm(s.pose(), T) < 1e-6
+        T = s.pose()  # continue both from the GPU pose so rounds stay comparable
+
+
+@pytest.mark.parametrize("n,seed,of,keep", [(10000, 10, 0.0, 0), (10000, 11, 0.3, 0),
+                                            (10000, 12, 0.3, 1), (100000, 13, 0.0, 0)])
+def test_solve_matches_oracle(native, oracle, n, seed, of, keep):
+    synth = _synth()
+    p = synth.make_problem(n, seed=seed, outlier_frac=of, pixel_noise=0.5)
+    s = native.PICPSolver()
+    s.init(p["T_init"], p["world"], p["image"])
+    s.setKernelThreshold(THR)
+    st = s.solve(p["pairs"], max_rounds=50, conv_eps=-1.0, keep_outliers=bool(keep))
+    T_ref, st_ref = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"],
+                                 THR, keep_outliers=keep, mode=oracle.MODE_F64, max_rounds=50,
+                                 conv_eps=-1.0)
+    T_f, _ = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"], THR,
+                          keep_outliers=keep, mode=oracle.MODE_FAITHFUL, max_rounds=50, conv_eps=-1.0)
+    assert st["rounds"] == 50 and st["ok"] == 1
+    assert synth.se3_log_norm(s.pose(), T_ref) < POSE_TOL
+    assert synth.se3_log_norm(s.pose(), T_f) < POSE_TOL
+    assert abs(st["n_in"] - st_ref["n_in"]) <= max(2, n // 10000)
+    assert synth.se3_log_norm(s.pose(), p["T_gt"]) < 1e-2
+
+
+def test_solve_convergence_rule_matches_oracle(native, oracle):
+    """exec/icp_test.cpp:99-106 evaluated on the device."""
+    synth = _synth()
+    p = synth.make_problem(3000, seed=21, pixel_noise=1.0)
+    s = native.PICPSolver()
+    s.init(p["T_init"], p["world"], p["image"])
+    s.setKernelThreshold(THR)
+    st = s.solve(p["pairs"], max_rounds=50, conv_eps=1e-3)
+    T_ref, st_ref = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"],
+                                 THR, mode=oracle.MODE_F64, max_rounds=50, conv_eps=1e-3)
+    assert st["converged"] == 1 and st_ref["converged"]
+    assert st["rounds"] == st_ref["rounds"]
+    assert synth.se3_log_norm(s.pose(), T_ref) < POSE_TOL
+
+
+def test_too_few_inliers_keeps_pose(native):
+    synth = _synth()
+    p = synth.make_problem(200, seed=3)
+    s = native.PICPSolver()
+    s.init(p["T_init"], p["world"], p["image"])
+    s._min_inliers = 1000  # src/picp_solver.cpp:97-100
+    assert s.oneRound(p["pairs"], False) is False
+    np.testing.assert_array_equal(s.pose(), p["T_init"])
+    st = s.solve(p["pairs"], max_rounds=50)
+    assert st["ok"] == 0 and st["rounds"] == 1
+    np.testing.assert_array_equal(s.pose(), p["T_init"])
+
+
+def test_empty_and_out_of_range(native):
+    synth = _synth()
+    p = synth.make_problem(50, seed=3)
+    s = native.PICPSolver()
+    s.init(p["T_init"], p["world"], p["image"])
+    st = s.solve(np.zeros((0, 2), np.int32), max_rounds=50)
+    assert st["n_in"] == 0 and st["ok"] == 1
+    np.testing.assert_array_equal(s.pose(), p["T_init"])  # H = I, b = 0 -> dx = 0
+    with pytest.raises(native.PicpError) as ei:
+        s.set_correspondences(np.array([[0, 50]], np.int32))
+    assert ei.value.code == native.ERR_RANGE
+    with pytest.raises(native.PicpError):
+        s.set_correspondences(np.array([[-1, 0]], np.int32))
+
+
+def test_points_behind_camera_and_outside_image_are_skipped(native, oracle):
+    synth = _synth()
+    p = synth.make_problem(2000, seed=8)
+    world = p["world"].copy()
+    # push a slice of points behind the camera and a slice far off-image
+    T = p["T_gt"].astype(np.float64)
+    cam = (T[:3, :3] @ world.T.astype(np.float64) + T[:3, 3:4]).T
+    cam[:100, 2] *= -1
+    cam[100:200, 0] += 50.0
+    Tcw = synth.rigid_inverse(T)
+    world = ((Tcw[:3, :3] @ cam.T) + Tcw[:3, 3:4]).T.astype(np.float32)
+    pairs = np.stack([np.arange(2000), np.arange(2000)], 1).astype(np.int32)
+    image = p["image"][p["pairs"][:, 0]]
+    world_p = world[p["pairs"][:, 1]]
+    s = native.PICPSolver()
+    s.init(p["T_init"], world_p, image)
+    s.setKernelThreshold(THR)
+    got = s.linearize(pairs)
+    ref = oracle.linearize(p["T_init"], p["K"], 480, 640, world_p, image, pairs, THR, mode=oracle.MODE_F64)
+    assert got["n_projected"] == ref["n_projected"] <= 1800
+    assert got["n_in"] == ref["n_in"]
+    _lin_close(got, ref)
+
+
+def test_batch_ragged_matches_single_and_oracle(native, oracle):
+    synth = _synth()
+    sizes = [0, 1, 3, 1000, 5000, 20001, 1024, 4097]
+    probs = [synth.make_problem(max(n, 1), seed=100 + i, outlier_frac=0.1, pixel_noise=0.5, shuffle=False)
+             for i, n in enumerate(sizes)]
+    xyz = np.concatenate([p["xyz"][:n] for p, n in zip(probs, sizes)])
+    uv = np.concatenate([p["uv"][:n] for p, n in zip(probs, sizes)])
+    b = native.Batch(sizes)
+    b.set_data(xyz, uv)
+    b.set_poses(np.stack([p["T_init"] for p in probs]))
+    b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
+    poses, stats = b.poses(), b.stats()
+    for i, (p, n) in enumerate(zip(probs, sizes)):
+        T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"][:n], p["y"][:n],
+                                         p["z"][:n], p["u"][:n], p["v"][:n], THR,
+                                         mode=oracle.MODE_F64, max_rounds=50, conv_eps=-1.0)
+        assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL, i
+        assert stats[i]["rounds"] == 50
+        if n >= 1000:
+            s = native.PICPSolver()
+            pr = np.stack([np.arange(n), np.arange(n)], 1).astype(np.int32)
+            s.init(p["T_init"], p["xyz"][:n], p["uv"][:n])
+            s.setKernelThreshold(THR)
+            s.solve(pr, max_rounds=50, conv_eps=-1.0)
+            # same partition and reduction order -> bit-identical to the batched solve
+            np.testing.assert_array_equal(s.pose(), poses[i])
+
+
+def test_solve_is_deterministic(native):
+    synth = _synth()
+    p = synth.make_problem(50000, seed=31, outlier_frac=0.3, pixel_noise=0.5)
+    out = []
+    for _ in range(2):
+        s = native.PICPSolver()
+        s.init(p["T_init"], p["world"], p["image"])
+        s.setKernelThreshold(THR)
+        st = s.solve(p["pairs"], max_rounds=50, conv_eps=-1.0)
+        out.append((s.pose(), st["chi_in"], st["n_in"]))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1:] == out[1][1:]
+
+
+def test_reference_data_kat_on_gpu(native, vo):
+    """All 120 data/ frames (batched, one problem per frame) converge to ground truth."""
+    synth = _synth()
+    sizes, xyz, uv, Ti = [], [], [], []
+    for k in range(1, vo.n_frames):
+        pr = vo.correspondences(k)
+        sizes.append(len(pr))
+        xyz.append(vo.world_xyz[pr[:, 1]])
+        uv.append(vo.frame(k)["uv"][pr[:, 0]])
+        Ti.append(vo.T_wc(k - 1))
+    b = native.Batch(sizes, K=vo.K)
+    b.set_data(np.concatenate(xyz), np.concatenate(uv))
+    b.set_poses(np.stack(Ti))
+    b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
+    P = b.poses()
+    worst = max(float(np.abs(P[k - 1] - vo.T_wc(k)).max()) for k in range(1, vo.n_frames))
+    assert worst < 1e-3, worst
+    for k, st in zip(range(1, vo.n_frames), b.stats()):
+        assert len(vo.correspondences(k)) - 2 <= st["n_in"]
+
+
+def test_drop_in_icp_loop_on_reference_data(native, oracle, vo):
+    """exec/icp_test.cpp:78-117 driven through oneRound (host loop), frames 1..10."""
+    synth = _synth()
+    s = native.PICPSolver(K=vo.K)
+    for k in range(1, 11):
+        pr = vo.correspondences(k)
+        s.init(vo.T_wc(k - 1), vo.world_xyz, vo.frame(k)["uv"])
+        s.setKernelThreshold(3000.0)
+        prev = np.finfo(np.float32).max
+        for j in range(50):
+            assert s.oneRound(pr, False)
+            cur = s.chiInliers()
+            rel = abs(prev - cur) / prev if prev > 1e-10 else 0.0
+            if rel < 1e-5:
+                break
+            prev = cur
+        T_ref, _ = oracle.solve(vo.T_wc(k - 1), vo.K, 480, 640, vo.world_xyz, vo.frame(k)["uv"], pr,
+                                3000.0, mode=oracle.MODE_F64)
+        assert synth.se3_log_norm(s.pose(), T_ref) < POSE_TOL
+        assert synth.se3_log_norm(s.pose(), vo.T_wc(k)) < 2e-3
+
+
+def test_triangulation_matches_oracle_and_world(native, oracle, vo):
+    g = np.load(os.path.join(GOLDEN, "picp_golden.npz"))
+    got = native.triangulate(g["tri/P1"], g["tri/P2"], g["tri/uv1"], g["tri/uv2"])
+    np.testing.assert_allclose(got, g["tri/xyz"], rtol=1e-5, atol=1e-5)
+    ref = vo.world_xyz[[int(np.where(vo.world_id == i)[0][0]) for i in g["tri/ids"]]]
+    assert np.abs(got - ref).max() < 2e-3
+    # random stress incl. near-degenerate rays, against the oracle
+    rng = np.random.default_rng(9)
+    uv1 = rng.uniform([0, 0], [639, 479], (5000, 2)).astype(np.float32)
+    uv2 = (uv1 + rng.normal(0, 3, uv1.shape)).astype(np.float32)
+    got = native.triangulate(g["tri/P1"], g["tri/P2"], uv1, uv2)
+    ref = oracle.triangulate(g["tri/P1"], g["tri/P2"], uv1, uv2)
+    rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1.0)
+    assert np.quantile(rel, 0.999) < 1e-4
+    assert native.triangulate(g["tri/P1"], g["tri/P2"], uv1[:0], uv2[:0]).shape == (0, 3)
+
+
+def test_projection_matrix_matches_oracle(native, oracle, vo):
+    Tcw = _synth().rigid_inverse(vo.T_wc(3).astype(np.float64)).astype(np.float32)
+    np.testing.assert_array_equal(native.projection_matrix(vo.K, Tcw), oracle.projection_matrix(vo.K, Tcw))
+
+
+def test_full_size_c2_c3_properties(native, oracle):
+    """BASELINE configs at full size: C2 (100k, 50 rounds) and C3 (1M, 30% outliers)."""
+    synth = _synth()
+    for n, of in ((100000, 0.0), (1000000, 0.3)):
+        p = synth.make_problem(n, seed=42, outlier_frac=of, pixel_noise=0.5)
+        b = native.Batch([n])
+        b.set_data(p["xyz"], p["uv"])
+        b.set_poses(p["T_init"][None])
+        b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
+        T = b.poses()[0]
+        st = b.stats()[0]
+        assert synth.se3_log_norm(T, p["T_gt"]) < 2e-3
+        # every true inlier is gated in; accidental outliers within sqrt(3000) px also pass
+        assert st["n_in"] >= int(0.99 * (n - p["outlier"].sum()))
+        T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"], p["y"], p["z"],
+                                         p["u"], p["v"], THR, mode=oracle.MODE_F64, max_rounds=50,
+                                         conv_eps=-1.0)
+        assert synth.se3_log_norm(T, T_ref) < POSE_TOL
+        assert abs(st["n_in"] - st_ref["n_in"]) <= 10

@@ -1,0 +1,232 @@
+"""CPU tests of the oracle (the parity checker) -- no GPU.
+
+Pins the oracle against the reference's own data: the data/ set is
+noise-free and exactly re-projectable, so (1) world.dat projected with a frame's gt pose
+reproduces its measurements, (2) PICP from the previous frame's gt pose converges to the
+current gt pose on all 120 frames, (3) DLT triangulation with gt poses reproduces world.dat.
+Also cross-checks the C restatement against an independent vectorised numpy restatement and
+freezes its outputs (tests/golden/picp_golden.npz).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+import sys
+sys.path.insert(0, GOLDEN)
+
+
+def _np_linearize(T, K, rows, cols, xyz, uv, thr, keep):
+    """Independent numpy restatement of src/picp_solver.cpp:26-91 (float32 per point, no
+    FMA: numpy evaluates each binary op with one rounding; float64 accumulation)."""
+    f = np.float32
+    T = T.astype(f)
+    K = K.astype(f)
+    x, y, z = xyz[:, 0].astype(f), xyz[:, 1].astype(f), xyz[:, 2].astype(f)
+    pc = [((T[i, 0] * x + T[i, 1] * y) + T[i, 2] * z) + T[i, 3] for i in range(3)]
+    ph = [((K[i, 0] * pc[0] + K[i, 1] * pc[1]) + K[i, 2] * pc[2]) for i in range(3)]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        iz = (f(1.0) / ph[2]).astype(f)
+        ix, iy = ph[0] * iz, ph[1] * iz
+    valid = ~(pc[2] <= 0) & ~((ix < 0) | (ix > f(cols - 1)) | (iy < 0) | (iy > f(rows - 1)))
+    e0, e1 = ix - uv[:, 0].astype(f), iy - uv[:, 1].astype(f)
+    chi = e0 * e0 + e1 * e1
+    out = chi > f(thr)
+    inl = valid & ~out
+    use = inl | (valid & bool(keep))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        lam = np.where(out, np.sqrt(f(thr) / chi), f(1.0)).astype(np.float64)
+    iz2 = iz.astype(np.float64) ** 2
+    izd = iz.astype(np.float64)
+    Jp = np.zeros((len(x), 2, 3))
+    Jp[:, 0, 0] = izd
+    Jp[:, 1, 1] = izd
+    Jp[:, 0, 2] = -ph[0] * iz2
+    Jp[:, 1, 2] = -ph[1] * iz2
+    pcd = np.stack(pc, 1).astype(np.float64)
+    S = np.zeros((len(x), 3, 3))  # skew(-pc)
+    m = -pcd
+    S[:, 0, 1], S[:, 0, 2] = -m[:, 2], m[:, 1]
+    S[:, 1, 0], S[:, 1, 2] = m[:, 2], -m[:, 0]
+    S[:, 2, 0], S[:, 2, 1] = -m[:, 1], m[:, 0]
+    Jr = np.concatenate([np.broadcast_to(np.eye(3), S.shape), S], 2)
+    J = Jp @ K.astype(np.float64) @ Jr
+    w = np.where(use, lam, 0.0)
+    e = np.stack([e0, e1], 1).astype(np.float64)
+    Ju, eu, wu = J[use], e[use], w[use]
+    H = np.einsum("n,nri,nrj->ij", wu, Ju, Ju)
+    b = np.einsum("n,nri,nr->i", wu, Ju, eu)
+    return {"H": H, "b": b, "chi_in": float(np.sum(chi[inl].astype(np.float64))),
+            "chi_out": float(np.sum(chi[valid & out].astype(np.float64))),
+            "n_in": int(inl.sum()), "n_projected": int(valid.sum())}
+
+
+def test_kat_projection_reproduces_measurement(oracle, vo):
+    # data/meas-00000.dat "point 0 6 522.119 187.968": world.dat point 6 seen at frame 0
+    ok, img = oracle.project_point(vo.T_wc(0), vo.K, vo.rows, vo.cols, vo.world_xyz[6])
+    assert ok
+    np.testing.assert_allclose(img, [522.119, 187.968], atol=2e-3)
+
+
+def test_kat_all_measurements_reproject(oracle, vo):
+    worst = 0.0
+    for k in range(vo.n_frames):
+        f = vo.frame(k)
+        pairs = vo.correspondences(k)
+        T = vo.T_wc(k)
+        for ii, wi in pairs[:: max(1, len(pairs) // 10)]:
+            ok, img = oracle.project_point(T, vo.K, vo.rows, vo.cols, vo.world_xyz[wi])
+            assert ok
+            worst = max(worst, float(np.abs(img - f["uv"][ii]).max()))
+    assert worst < 0.05, worst  # gt poses are stored with 6 significant digits
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kat_picp_converges_to_ground_truth_on_reference_data(oracle, vo, mode):
+    """icp_test's PICP (threshold 3000, 50 rounds) from gt pose k-1 lands on gt pose k."""
+    worst = 0.0
+    for k in range(1, vo.n_frames):
+        pairs = vo.correspondences(k)
+        T, st = oracle.solve(vo.T_wc(k - 1), vo.K, vo.rows, vo.cols, vo.world_xyz,
+                             vo.frame(k)["uv"], pairs, 3000.0, mode=mode)
+        # every projectable point is an inlier; points the simulator put at x in (639, 640)
+        # are rejected by the reference's `x > cols-1` bound (src/camera.h:31), <= 2 per frame
+        assert st["ok"] == 1 and len(pairs) - 2 <= st["n_in"] <= len(pairs)
+        worst = max(worst, float(np.abs(T - vo.T_wc(k)).max()))
+    assert worst < 1e-3, worst  # 5.7e-4 (float32 noise floor)
+
+
+def test_kat_triangulation_reproduces_world(oracle, vo):
+    g = np.load(os.path.join(GOLDEN, "picp_golden.npz"))
+    xyz = oracle.triangulate(g["tri/P1"], g["tri/P2"], g["tri/uv1"], g["tri/uv2"])
+    ids = g["tri/ids"]
+    ref = vo.world_xyz[[int(np.where(vo.world_id == i)[0][0]) for i in ids]]
+    assert len(ids) > 20
+    assert np.abs(xyz - ref).max() < 2e-3  # 2.6e-4 on frames 0/5
+
+
+def test_triangulation_matches_numpy_svd(oracle):
+    rng = np.random.default_rng(5)
+    K = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
+    from picp_amd import synth
+    T1 = synth.rigid_inverse(synth.world_in_camera((0, 0, 0.1)))
+    T2 = synth.rigid_inverse(synth.world_in_camera((0.5, 0.2, 0.2)))
+    P1 = oracle.projection_matrix(K, T1.astype(np.float32))
+    P2 = oracle.projection_matrix(K, T2.astype(np.float32))
+    uv1 = rng.uniform([0, 0], [639, 479], (200, 2)).astype(np.float32)
+    uv2 = rng.uniform([0, 0], [639, 479], (200, 2)).astype(np.float32)
+    got = oracle.triangulate(P1, P2, uv1, uv2)
+    for i in range(200):
+        A = np.zeros((4, 4))
+        for j, (P, uv) in enumerate(((P1, uv1[i]), (P2, uv2[i]))):
+            A[2 * j] = uv[0] * P[2].astype(np.float64) - P[0]
+            A[2 * j + 1] = uv[1] * P[2].astype(np.float64) - P[1]
+        X = np.linalg.svd(A)[2][-1].astype(np.float32)
+        w = X[3]
+        ref = X[:3] * (np.float32(1) / w if abs(w) > np.finfo(np.float32).eps else 1)
+        np.testing.assert_allclose(got[i], ref, rtol=2e-4, atol=1e-4)
+
+
+def test_ldlt_matches_numpy(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        M = rng.normal(size=(6, 6))
+        A = M @ M.T + np.eye(6)
+        r = rng.normal(size=6)
+        np.testing.assert_allclose(oracle.ldlt_solve6(A, r), np.linalg.solve(A, r), rtol=1e-10)
+        xf = oracle.ldlt_solve6(A.astype(np.float32), r.astype(np.float32), double=False)
+        np.testing.assert_allclose(xf, np.linalg.solve(A, r), rtol=2e-3, atol=1e-4)
+
+
+def test_v2t_euler_matches_rx_ry_rz(oracle):
+    from picp_amd.synth import euler_xyz
+    v = np.array([0.1, -0.2, 0.3, 0.05, -0.07, 0.11], np.float32)
+    T = oracle.v2t_euler(v)
+    np.testing.assert_allclose(T[:3, :3], euler_xyz(*v[3:].astype(np.float64)), atol=1e-6)
+    np.testing.assert_allclose(T[:3, 3], v[:3])
+    np.testing.assert_allclose(T[3], [0, 0, 0, 1])
+
+
+def test_jacobian_matches_finite_differences(oracle):
+    """J is the derivative of the projection under the left update T <- v2tEuler(dx)*T."""
+    from picp_amd import synth
+    p = synth.make_problem(5, seed=3)
+    T = p["T_gt"].astype(np.float64)
+    K = p["K"].astype(np.float64)
+    for wi in range(5):
+        X = p["world"][wi].astype(np.float64)
+
+        def proj(dx):
+            D = np.eye(4)
+            D[:3, :3] = synth.euler_xyz(*dx[3:])
+            D[:3, 3] = dx[:3]
+            pc = (D @ T)[:3, :3] @ X + (D @ T)[:3, 3]
+            ph = K @ pc
+            return ph[:2] / ph[2]
+
+        z = proj(np.zeros(6)).astype(np.float32)
+        ok, e, J = oracle.error_and_jacobian(p["T_gt"], p["K"], 480, 640, p["world"][wi], z)
+        if not ok:
+            continue
+        h = 1e-6
+        Jn = np.stack([(proj(h * np.eye(6)[i]) - proj(-h * np.eye(6)[i])) / (2 * h) for i in range(6)], 1)
+        np.testing.assert_allclose(J, Jn, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("keep", [0, 1])
+@pytest.mark.parametrize("of", [0.0, 0.3])
+def test_oracle_matches_independent_numpy_restatement(oracle, keep, of):
+    from picp_amd import synth
+    p = synth.make_problem(3000, seed=11, outlier_frac=of, pixel_noise=0.5)
+    lin = oracle.linearize(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"],
+                           3000.0, keep_outliers=keep, mode=oracle.MODE_F64)
+    ref = _np_linearize(p["T_init"], p["K"], 480, 640, p["xyz"], p["uv"], 3000.0, keep)
+    assert lin["n_in"] == ref["n_in"] and lin["n_projected"] == ref["n_projected"]
+    np.testing.assert_allclose(lin["chi_in"], ref["chi_in"], rtol=1e-9)
+    np.testing.assert_allclose(lin["chi_out"], ref["chi_out"], rtol=1e-9)
+    scale = np.abs(ref["H"]).max()
+    np.testing.assert_allclose(lin["H"], ref["H"], rtol=1e-4, atol=1e-5 * scale)
+    np.testing.assert_allclose(lin["b"], ref["b"], rtol=1e-4, atol=1e-5 * np.abs(ref["b"]).max())
+
+
+def test_faithful_and_f64_modes_agree(oracle):
+    from picp_amd import synth
+    p = synth.make_problem(20000, seed=4, pixel_noise=0.5, outlier_frac=0.1)
+    Tf, sf = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"], 3000.0,
+                          mode=oracle.MODE_FAITHFUL, conv_eps=-1)
+    Td, sd = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"], 3000.0,
+                          mode=oracle.MODE_F64, conv_eps=-1)
+    assert synth.se3_log_norm(Tf, Td) < 1e-5
+    assert synth.se3_log_norm(Td, p["T_gt"]) < 2e-3
+
+
+def test_min_inliers_failure_keeps_pose(oracle):
+    from picp_amd import synth
+    p = synth.make_problem(100, seed=1)
+    ok, T, st = oracle.one_round(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"],
+                                 3000.0, min_inliers=1000)
+    assert not ok
+    np.testing.assert_array_equal(T, p["T_init"])
+
+
+def test_golden_vectors_regression(oracle):
+    """The oracle reproduces its committed outputs bit for bit (deterministic C)."""
+    from picp_amd import synth
+    sys_cases = __import__("make_golden").CASES
+    g = np.load(os.path.join(GOLDEN, "picp_golden.npz"))
+    for name, n, seed, of, noise in sys_cases:
+        p = synth.make_problem(n, seed=seed, outlier_frac=of, pixel_noise=noise)
+        np.testing.assert_array_equal(__import__("make_golden").checksum(p), g[name + "/checksum"])
+        if name + "/world" in g:
+            np.testing.assert_array_equal(p["world"], g[name + "/world"])
+            np.testing.assert_array_equal(p["pairs"], g[name + "/pairs"])
+        for keep in (0, 1):
+            lin = oracle.linearize(p["T_init"], p["K"], 480, 640, p["world"], p["image"],
+                                   p["pairs"], 3000.0, keep_outliers=keep, mode=oracle.MODE_F64)
+            tag = "%s/lin_keep%d" % (name, keep)
+            np.testing.assert_array_equal(lin["H"], g[tag + "/H"])
+            np.testing.assert_array_equal(lin["b"], g[tag + "/b"])
+        T, st = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"],
+                             3000.0, mode=oracle.MODE_F64, max_rounds=50, conv_eps=-1.0)
+        np.testing.assert_array_equal(T, g["%s/solve_f64/T" % name])
