@@ -5,8 +5,9 @@
 //   planes X,Y,Z,U,V : float32 SoA, one plane each, problem p occupies
 //                      [prob.offset, prob.offset + prob.n) of every plane; offsets are
 //                      multiples of 4 floats so every block streams float4 (dwordx4) loads.
-//   PicpProblem[np]  : per-problem constants (camera, gate, damping, loop controls).
-//   int4 blkinfo[nb] : linearize block -> (problem, first item, item count).
+//   PicpArgs         : batch-wide camera/gate/loop parameters, by-value kernel argument.
+//   PicpProblem[np]  : ragged batches only: per-problem partition.
+//   int4 blkinfo[nb] : ragged batches only: block -> (problem, first item, item count).
 //   PicpState[2][np] : ping-pong per-problem solver state (pose + icp_test loop state).
 //   float part[2][nb][32] : ping-pong per-block partial sums of the normal equations.
 #pragma once
@@ -22,20 +23,30 @@
 #define PICP_P_N_IN 29
 #define PICP_P_N_PROJ 30
 
+// Ragged batches only: per-problem partition (uniform batches compute it from blockIdx).
 struct PicpProblem {
   int64_t offset;      // first item in the SoA planes (multiple of 4)
   int32_t n;           // number of correspondences
   int32_t blk0;        // first linearize block (index into partials) of this problem
   int32_t nblk;        // number of linearize blocks (>= 1)
-  int32_t rows, cols;  // image size (src/camera.h:43-44)
-  float K[9];          // camera matrix, column-major
-  float threshold;     // kernel threshold (src/picp_solver.h:72)
-  float damping;       // src/picp_solver.h:73
-  int32_t min_inliers; // src/picp_solver.h:74
-  int32_t keep_outliers;
-  int32_t max_rounds;  // exec/icp_test.cpp:88
-  float conv_eps;      // exec/icp_test.cpp:91 (negative: never converge)
-  int32_t pad[2];
+  int32_t pad;
+};
+
+// Batch-wide launch arguments, passed BY VALUE (kernel-argument SGPRs: no memory hop).
+struct PicpArgs {
+  float K[9];            // camera matrix, column-major (src/camera.h:45)
+  float maxx, maxy;      // cols-1, rows-1 (src/camera.h:31,33)
+  float threshold;       // kernel threshold (src/picp_solver.h:72)
+  float damping;         // src/picp_solver.h:73
+  float conv_eps;        // exec/icp_test.cpp:91 (negative: never converge)
+  int32_t min_inliers;   // src/picp_solver.h:74
+  int32_t keep_outliers; // oneRound's keep_outliers
+  int32_t max_rounds;    // exec/icp_test.cpp:88
+  int32_t uniform;       // 1: problem p = block / nblk_u, items at p*stride_u (no tables)
+  int32_t n_u;           // uniform: correspondences per problem
+  int32_t nblk_u;        // uniform: blocks per problem
+  int32_t ipb;           // items per linearize block
+  int64_t stride_u;      // uniform: plane stride between problems (multiple of 4)
 };
 
 // 128-byte per-problem solver state

@@ -21,6 +21,23 @@
 
 #include "picp_internal.h"
 
+// Diagnostic build only (-DPICP_STAMPS, lib/libpicp_amd_stamps.so): thread 0 of each block
+// records s_memrealtime (100 MHz) at phase boundaries of launches j = 10 and 11 into a buffer
+// nothing else reads.  The shipped library compiles these to nothing.
+#ifdef PICP_STAMPS
+#define PICP_STAMP_BLOCKS 4096
+__device__ unsigned long long picp_stamps[2][PICP_STAMP_BLOCKS][8];
+#define STAMP(k)                                                                         \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && !finalize && (j == 10 || j == 11) && blockIdx.x < PICP_STAMP_BLOCKS) \
+      picp_stamps[j - 10][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();              \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 namespace picp {
 
 struct Pose {
@@ -129,68 +146,115 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
   }
 }
 
-// One halving-butterfly step over 2*HALF values: lanes l and l^M exchange the half the
-// other keeps, so the number of live values per lane halves per step (32 -> 1 in five
-// steps, 32 cross-lane moves in total instead of 6*32 for a naive per-value tree).
-template <int M, int HALF>
-__device__ __forceinline__ void bfly(float* v, int lane) {
-  const bool hi = (lane & M) != 0;
+// Cross-lane moves without the LDS crossbar.  gfx950 v_permlane32_swap / v_permlane16_swap
+// exchange half-waves / odd-even 16-lane rows between two registers; DPP reads a partner
+// lane inside a 16-lane row (row_mirror l^15, row_half_mirror l^7, quad_perm l^2, l^1).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+#define DPP_ROW_MIRROR 0x140
+#define DPP_ROW_HALF_MIRROR 0x141
+#define DPP_QUAD_XOR2 0x4E  // quad_perm [2,3,0,1]
+#define DPP_QUAD_XOR1 0xB1  // quad_perm [1,0,3,2]
+
+// Halving-butterfly step inside a 16-lane row: lanes l and P(l) (P an involution that flips
+// bit HB) exchange the half of the 2*HALF values the other keeps.
+template <int CTRL, int HB, int HALF>
+__device__ __forceinline__ void bfly_dpp(float* v, int lane) {
+  const bool hi = (lane >> HB) & 1;
 #pragma unroll
   for (int i = 0; i < HALF; ++i) {
     const float send = hi ? v[i] : v[i + HALF];
     const float keep = hi ? v[i + HALF] : v[i];
-    v[i] = keep + __shfl_xor(send, M, 64);
+    v[i] = keep + dpp<CTRL>(send);
   }
 }
 
-// Sum 32 per-lane values over the 64 lanes of a wave.  Returns, in every lane, the wave
-// total of value index (lane >> 1).
+// Sum 32 per-lane values over the 64 lanes of a wave (32 -> 16 -> 8 -> 4 -> 2 -> 1 values per
+// lane).  The swap steps need no select: after v_permlane32_swap(a=v[i], b=v[i+16]) the low
+// half holds (own v[i], partner v[i]) and the high half (partner v[i+16], own v[i+16]), so a+b
+// is the pair sum of the half each lane keeps.  Returns, in every lane, the wave total of value
+// index (lane >> 1).
 __device__ __forceinline__ float wave_reduce32(float* v, int lane) {
-  bfly<32, 16>(v, lane);
-  bfly<16, 8>(v, lane);
-  bfly<8, 4>(v, lane);
-  bfly<4, 2>(v, lane);
-  bfly<2, 1>(v, lane);
-  return v[0] + __shfl_xor(v[0], 1, 64);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 16]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  bfly_dpp<DPP_ROW_MIRROR, 3, 4>(v, lane);
+  bfly_dpp<DPP_ROW_HALF_MIRROR, 2, 2>(v, lane);
+  bfly_dpp<DPP_QUAD_XOR2, 1, 1>(v, lane);
+  return v[0] + dpp<DPP_QUAD_XOR1>(v[0]);
 }
 
-// Damped normal equations -> dx, plain LDL^T (H + damping*I is SPD) in double, fully
-// unrolled so everything stays in registers.  Eigen's LDLT (src/picp_solver.cpp:102) adds
-// diagonal pivoting, which only changes rounding for an SPD matrix; the zero-pivot rule
-// (|d| <= DBL_MIN -> component 0) is Eigen's.
-__device__ __forceinline__ void ldlt6_solve(double A[6][6], const double rhs[6], double x[6]) {
-  double L[6][6], D[6];
+// 1/d in float: hardware v_rcp_f32 estimate refined by one Newton step (<= 1 ulp for normal
+// d); |d| <= FLT_MIN -> 0 (Eigen's LDLT zero-pivot rule for float, src/picp_solver.cpp:102).
+__device__ __forceinline__ float rcp32(float d) {
+  float r = __builtin_amdgcn_rcpf(d);
+  r = fmaf(r, fmaf(-d, r, 1.0f), r);
+  return (fabsf(d) > FLT_MIN) ? r : 0.0f;
+}
+
+// Damped normal equations -> dx.  float32 LDL^T, the precision the reference solves in
+// (Matrix6f::ldlt, src/picp_solver.cpp:102); H and b arrive as exact double sums.  Plain LDL^T
+// without Eigen's diagonal pivoting (H + damping*I is SPD: pivoting only changes rounding).
+// Fully unrolled: registers only, one lane.
+__device__ __forceinline__ void ldlt6_solve(float A[6][6], const float rhs[6], float x[6]) {
+  float L[6][6], D[6], iD[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
-    double d = A[j][j];
+    float d = A[j][j];
+    float LD[6];
 #pragma unroll
-    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
+    for (int k = 0; k < j; ++k) {
+      LD[k] = L[j][k] * D[k];
+      d = fmaf(-LD[k], L[j][k], d);
+    }
     D[j] = d;
-    const double id = (fabs(d) > 0.0) ? 1.0 / d : 0.0;
+    iD[j] = rcp32(d);
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
-      double s = A[i][j];
+      float s = A[i][j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k] * D[k];
-      L[i][j] = s * id;
+      for (int k = 0; k < j; ++k) s = fmaf(-L[i][k], LD[k], s);
+      L[i][j] = s * iD[j];
     }
   }
-  double y[6];
+  float y[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    double s = rhs[i];
+    float s = rhs[i];
 #pragma unroll
-    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+    for (int k = 0; k < i; ++k) s = fmaf(-L[i][k], y[k], s);
     y[i] = s;
   }
 #pragma unroll
-  for (int i = 0; i < 6; ++i) y[i] = (fabs(D[i]) > DBL_MIN) ? y[i] / D[i] : 0.0;
+  for (int i = 0; i < 6; ++i) y[i] *= iD[i];
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
-    double s = y[i];
+    float s = y[i];
 #pragma unroll
-    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+    for (int k = i + 1; k < 6; ++k) s = fmaf(-L[k][i], x[k], s);
     x[i] = s;
+  }
+}
+
+// sin/cos of a GN increment angle.  Increments are small, so the float Taylor series (exact to
+// float rounding for |a| <= 1/16: next term a^9/9! < 1e-16) avoids sincosf's range reduction
+// on the single-lane critical path; larger angles take the libm path.
+__device__ __forceinline__ void small_sincos(float a, float* s, float* c) {
+  if (fabsf(a) <= 0.0625f) {
+    const float a2 = a * a;
+    *s = a * fmaf(a2, fmaf(a2, fmaf(a2, -1.0f / 5040.0f, 1.0f / 120.0f), -1.0f / 6.0f), 1.0f);
+    *c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 1.0f / 40320.0f, -1.0f / 720.0f), 1.0f / 24.0f), -0.5f), 1.0f);
+  } else {
+    sincosf(a, s, c);
   }
 }
 
@@ -198,9 +262,9 @@ __device__ __forceinline__ void ldlt6_solve(double A[6][6], const double rhs[6],
 // src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
 __device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
   float sa, ca, sb, cb, sc, cc;
-  sincosf(dx[3], &sa, &ca);
-  sincosf(dx[4], &sb, &cb);
-  sincosf(dx[5], &sc, &cc);
+  small_sincos(dx[3], &sa, &ca);
+  small_sincos(dx[4], &sb, &cb);
+  small_sincos(dx[5], &sc, &cc);
   const float Rx[3][3] = {{1.f, 0.f, 0.f}, {0.f, ca, -sa}, {0.f, sa, ca}};
   const float Ry[3][3] = {{cb, 0.f, sb}, {0.f, 1.f, 0.f}, {-sb, 0.f, cb}};
   const float Rz[3][3] = {{cc, -sc, 0.f}, {sc, cc, 0.f}, {0.f, 0.f, 1.f}};
@@ -244,86 +308,177 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
   for (int i = 0; i < 3; ++i) t[i] = tn[i];
 }
 
-// Finish round (j-1) of problem p from its block partials: H, b, stats -> new state.
+// Finish round (j-1) of a problem from its block-partial totals: H, b, stats -> new state.
 // Runs in one lane; everything is indexed by compile-time constants.
-__device__ void finish_round(const PicpProblem& P, const PicpState& s, const double* tot,
-                             int j, PicpState& ns) {
+__device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState& s,
+                                             const double* tot, int j, PicpState& ns) {
   ns = s;
   ns.chi_in = (float)tot[PICP_P_CHI_IN];
   ns.chi_out = (float)tot[PICP_P_CHI_OUT];
   ns.n_in = (int32_t)tot[PICP_P_N_IN];
   ns.n_proj = (int32_t)tot[PICP_P_N_PROJ];
   ns.rounds = j;
-  double H[6][6];
+  float H[6][6];
   int k = 0;
 #pragma unroll
   for (int r = 0; r < 6; ++r)
 #pragma unroll
     for (int c = r; c < 6; ++c) {
-      H[r][c] = tot[PICP_P_H + k];
-      H[c][r] = tot[PICP_P_H + k];
+      const double h = tot[PICP_P_H + k] + ((r == c) ? (double)A.damping : 0.0);  // :96
+      H[r][c] = (float)h;
+      H[c][r] = (float)h;
       ++k;
     }
-#pragma unroll
-  for (int r = 0; r < 6; ++r) H[r][r] += (double)P.damping;  // src/picp_solver.cpp:96
-  if (ns.n_in < P.min_inliers) {                              // :97-100
+  if (ns.n_in < A.min_inliers) {  // src/picp_solver.cpp:97-100
     ns.ok = 0;
     ns.done = 1;
     return;
   }
-  double nb[6], dxd[6];
+  float nb[6], dx[6];
 #pragma unroll
-  for (int r = 0; r < 6; ++r) nb[r] = -tot[PICP_P_B + r];
-  ldlt6_solve(H, nb, dxd);  // :102
-  float dx[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) dx[r] = (float)dxd[r];
+  for (int r = 0; r < 6; ++r) nb[r] = (float)(-tot[PICP_P_B + r]);
+  ldlt6_solve(H, nb, dx);        // :102
   apply_update(dx, ns.R, ns.t);  // :103
   ns.ok = 1;
   // exec/icp_test.cpp:99-106
   const float prev = s.chi_prev, cur = ns.chi_in;
   const float rel = (prev > 1e-10f) ? fabsf(prev - cur) / prev : 0.0f;
-  if (rel < P.conv_eps) {
+  if (rel < A.conv_eps) {
     ns.converged = 1;
     ns.done = 1;
   } else {
     ns.chi_prev = cur;
   }
-  if (j >= P.max_rounds) ns.done = 1;
+  if (j >= A.max_rounds) ns.done = 1;
 }
 
 }  // namespace picp
 
 using namespace picp;
 
+// Deterministic sum of a problem's block partials (nblk x 32 floats) in double.  Lane t reads
+// float4 quad (t & 7) of blocks (t >> 3) + 32*u: all PICP_RED_UNROLL loads of a sweep are
+// issued before the first add (out-of-range slots re-read the last block and are masked, so
+// no load sits behind a branch), i.e. one memory latency per 32*PICP_RED_UNROLL blocks.  Then a
+// fixed-order LDS combine.  Result in s_tot[0..31]; all threads call; ends with a barrier.
+#define PICP_RED_UNROLL 16
+__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int blk0, int nblk,
+                                                double (*s_red)[PICP_NPART + 1], double* s_tot,
+                                                int32_t* st_slot, int32_t st_word) {
+  const int tid = threadIdx.x;
+  const int q = tid & 7, r = tid >> 3;  // PICP_BLOCK/8 = 32 block slots per sweep
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  const float4* p4 = reinterpret_cast<const float4*>(part + (size_t)blk0 * PICP_NPART) + q;
+  for (int base = 0; base < nblk; base += 32 * PICP_RED_UNROLL) {
+    float4 v[PICP_RED_UNROLL];
+#pragma unroll
+    for (int u = 0; u < PICP_RED_UNROLL; ++u) {
+      const int bb = min(base + u * 32 + r, nblk - 1);
+      v[u] = p4[(size_t)bb * (PICP_NPART / 4)];
+    }
+#pragma unroll
+    for (int u = 0; u < PICP_RED_UNROLL; ++u) {
+      const bool ok = base + u * 32 + r < nblk;
+      a0 += ok ? (double)v[u].x : 0.0;
+      a1 += ok ? (double)v[u].y : 0.0;
+      a2 += ok ? (double)v[u].z : 0.0;
+      a3 += ok ? (double)v[u].w : 0.0;
+    }
+  }
+  s_red[r][4 * q + 0] = a0;
+  s_red[r][4 * q + 1] = a1;
+  s_red[r][4 * q + 2] = a2;
+  s_red[r][4 * q + 3] = a3;
+  if (st_slot) *st_slot = st_word;
+  __syncthreads();
+  if (tid < PICP_NPART) {
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 32; k += 4) {
+      t0 += s_red[k + 0][tid];
+      t1 += s_red[k + 1][tid];
+      t2 += s_red[k + 2][tid];
+      t3 += s_red[k + 3][tid];
+    }
+    s_tot[tid] = (t0 + t1) + (t2 + t3);
+  }
+  __syncthreads();
+}
+
 // Launch j (0 <= j <= R) of the fused R-round solve.  Launch j finishes round j-1 (j>0) and,
 // unless the problem is done, linearizes round j.  With finalize=1 only the finishing part
 // runs, one block per problem.  State and partials ping-pong between launches, so no
 // inter-workgroup synchronisation is ever needed inside a launch: the kernel boundary is the
-// only hand-off.
-extern "C" __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
+// only hand-off.  VEC = correspondences per lane per chunk (4: float4 loads, for large
+// batches; 1: one per lane, to spread a single frame over every SIMD).
+template <int VEC>
+__global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-    const float* __restrict__ U, const float* __restrict__ V,
+    const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const int4* __restrict__ blkinfo,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
     const float* __restrict__ part_in, float* __restrict__ part_out, int j, int finalize) {
-  __shared__ double s_red[8][PICP_NPART];
+  __shared__ double s_red[32][PICP_NPART + 1];
+  __shared__ double s_tot[PICP_NPART];
   __shared__ float s_wave[PICP_BLOCK / 64][PICP_NPART];
   __shared__ float s_pose[12];
+  __shared__ int32_t s_state[32];
   __shared__ int s_go;
 
   const int tid = threadIdx.x;
-  int p, first = 0, count = 0;
-  if (finalize) {
-    p = blockIdx.x;
+  STAMP(0);
+  int p, first = 0, count = 0, blk0, nblk;
+  int64_t base;
+  if (A.uniform) {
+    p = finalize ? (int)blockIdx.x : (int)blockIdx.x / A.nblk_u;
+    const int kb = (int)blockIdx.x - p * A.nblk_u;
+    first = kb * A.ipb;
+    count = max(0, min(A.ipb, A.n_u - first));
+    blk0 = p * A.nblk_u;
+    nblk = A.nblk_u;
+    base = (int64_t)p * A.stride_u + first;
   } else {
-    const int4 bi = blkinfo[blockIdx.x];
-    p = bi.x;
-    first = bi.y;
-    count = bi.z;
+    if (finalize) {
+      p = blockIdx.x;
+    } else {
+      const int4 bi = blkinfo[blockIdx.x];
+      p = bi.x;
+      first = bi.y;
+      count = bi.z;
+    }
+    const PicpProblem P = probs[p];
+    blk0 = P.blk0;
+    nblk = P.nblk;
+    base = P.offset + first;
   }
-  const PicpProblem& P = probs[p];
-  const bool leader = finalize || ((int)blockIdx.x == P.blk0);
+  const bool leader = finalize || ((int)blockIdx.x == blk0);
+
+  // Prefetch this lane's first chunk of every plane: the loads do not depend on the pose, so
+  // their latency overlaps the prologue below.
+  float xs[VEC], ys[VEC], zs[VEC], us[VEC], vs[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) xs[k] = ys[k] = zs[k] = us[k] = vs[k] = 0.0f;
+  const int c0 = tid * VEC;
+  if (!finalize && c0 < count) {
+    if constexpr (VEC == 4) {
+      const float4 x4 = *reinterpret_cast<const float4*>(X + base + c0);
+      const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c0);
+      const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c0);
+      const float4 u4 = *reinterpret_cast<const float4*>(U + base + c0);
+      const float4 v4 = *reinterpret_cast<const float4*>(V + base + c0);
+      xs[0] = x4.x; xs[1] = x4.y; xs[2] = x4.z; xs[3] = x4.w;
+      ys[0] = y4.x; ys[1] = y4.y; ys[2] = y4.z; ys[3] = y4.w;
+      zs[0] = z4.x; zs[1] = z4.y; zs[2] = z4.z; zs[3] = z4.w;
+      us[0] = u4.x; us[1] = u4.y; us[2] = u4.z; us[3] = u4.w;
+      vs[0] = v4.x; vs[1] = v4.y; vs[2] = v4.z; vs[3] = v4.w;
+    } else {
+      xs[0] = X[base + c0];
+      ys[0] = Y[base + c0];
+      zs[0] = Z[base + c0];
+      us[0] = U[base + c0];
+      vs[0] = V[base + c0];
+    }
+  }
 
   if (j == 0) {
     if (tid < 12) s_pose[tid] = (tid < 9) ? st_in[p].R[tid] : st_in[p].t[tid - 9];
@@ -333,49 +488,42 @@ extern "C" __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
       s.chi_in = s.chi_out = 0.0f;
       s.n_in = s.n_proj = 0;
       s.rounds = 0;
-      s.done = (P.max_rounds <= 0) ? 1 : 0;
+      s.done = (A.max_rounds <= 0) ? 1 : 0;
       s.ok = 1;
       s.converged = 0;
       if (leader) st_out[p] = s;
       s_go = !s.done;
     }
   } else {
-    const PicpState& s_in = st_in[p];
+    // The state (128 B -> LDS) and the previous round's partials are independent loads: issue
+    // both before waiting on either.  The partials of a finished problem are stale but unused.
+    int32_t st_word = 0;
+    if (tid < 32) st_word = reinterpret_cast<const int32_t*>(st_in + p)[tid];
+    STAMP(1);
+    reduce_partials(part_in, blk0, nblk, s_red, s_tot, tid < 32 ? &s_state[tid] : nullptr, st_word);
+    STAMP(2);
+    const PicpState& s_in = *reinterpret_cast<const PicpState*>(s_state);
     if (s_in.done) {  // finished earlier: propagate the state through the ping-pong
-      if (leader && tid < 32)
-        reinterpret_cast<int32_t*>(&st_out[p])[tid] =
-            reinterpret_cast<const int32_t*>(&s_in)[tid];
+      if (leader && tid < 32) reinterpret_cast<int32_t*>(&st_out[p])[tid] = s_state[tid];
       return;
     }
-    // deterministic reduction of the previous round's partials, fixed order, in double
-    const int e = tid & 31, g = tid >> 5;
-    double acc = 0.0;
-    const float* pp = part_in + (size_t)P.blk0 * PICP_NPART + e;
-    for (int b = g; b < P.nblk; b += PICP_BLOCK / 32) acc += (double)pp[(size_t)b * PICP_NPART];
-    s_red[g][e] = acc;
-    __syncthreads();
-    if (tid < 32) {
-      double tsum = 0.0;
-#pragma unroll
-      for (int gg = 0; gg < PICP_BLOCK / 32; ++gg) tsum += s_red[gg][tid];
-      s_red[0][tid] = tsum;
-    }
-    __syncthreads();
     if (tid == 0) {
       double tot[PICP_NPART];
 #pragma unroll
-      for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_red[0][i];
+      for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
       PicpState ns;
-      finish_round(P, s_in, tot, j, ns);
-      if (leader) st_out[p] = ns;
+      finish_round(A, s_in, tot, j, ns);
+      STAMP(6);
 #pragma unroll
       for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
 #pragma unroll
       for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
       s_go = !ns.done;
+      if (leader) st_out[p] = ns;
     }
   }
   __syncthreads();
+  STAMP(3);
   if (finalize || !s_go) return;
 
   // ---------------- linearize (src/picp_solver.cpp:56-91) ----------------
@@ -385,13 +533,13 @@ extern "C" __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
   T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
   Cam C;
-  C.k00 = P.K[0]; C.k10 = P.K[1]; C.k20 = P.K[2];
-  C.k01 = P.K[3]; C.k11 = P.K[4]; C.k21 = P.K[5];
-  C.k02 = P.K[6]; C.k12 = P.K[7]; C.k22 = P.K[8];
-  C.maxx = (float)(P.cols - 1);
-  C.maxy = (float)(P.rows - 1);
-  const float thr = P.threshold;
-  const bool keep = P.keep_outliers != 0;
+  C.k00 = A.K[0]; C.k10 = A.K[1]; C.k20 = A.K[2];
+  C.k01 = A.K[3]; C.k11 = A.K[4]; C.k21 = A.K[5];
+  C.k02 = A.K[6]; C.k12 = A.K[7]; C.k22 = A.K[8];
+  C.maxx = A.maxx;
+  C.maxy = A.maxy;
+  const float thr = A.threshold;
+  const bool keep = A.keep_outliers != 0;
 
   Acc a;
 #pragma unroll
@@ -400,20 +548,33 @@ extern "C" __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
   a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
 
-  const int64_t base = P.offset + first;
-  for (int c = tid * 4; c < count; c += PICP_BLOCK * 4) {
-    const float4 x4 = *reinterpret_cast<const float4*>(X + base + c);
-    const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c);
-    const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c);
-    const float4 u4 = *reinterpret_cast<const float4*>(U + base + c);
-    const float4 v4 = *reinterpret_cast<const float4*>(V + base + c);
+  for (int c = c0; c < count; c += PICP_BLOCK * VEC) {
+    if (c != c0) {  // chunks after the prefetched one
+      if constexpr (VEC == 4) {
+        const float4 x4 = *reinterpret_cast<const float4*>(X + base + c);
+        const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c);
+        const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c);
+        const float4 u4 = *reinterpret_cast<const float4*>(U + base + c);
+        const float4 v4 = *reinterpret_cast<const float4*>(V + base + c);
+        xs[0] = x4.x; xs[1] = x4.y; xs[2] = x4.z; xs[3] = x4.w;
+        ys[0] = y4.x; ys[1] = y4.y; ys[2] = y4.z; ys[3] = y4.w;
+        zs[0] = z4.x; zs[1] = z4.y; zs[2] = z4.z; zs[3] = z4.w;
+        us[0] = u4.x; us[1] = u4.y; us[2] = u4.z; us[3] = u4.w;
+        vs[0] = v4.x; vs[1] = v4.y; vs[2] = v4.z; vs[3] = v4.w;
+      } else {
+        xs[0] = X[base + c];
+        ys[0] = Y[base + c];
+        zs[0] = Z[base + c];
+        us[0] = U[base + c];
+        vs[0] = V[base + c];
+      }
+    }
     const int rem = count - c;
-    accumulate_one(T, C, thr, keep, x4.x, y4.x, z4.x, u4.x, v4.x, rem > 0, a);
-    accumulate_one(T, C, thr, keep, x4.y, y4.y, z4.y, u4.y, v4.y, rem > 1, a);
-    accumulate_one(T, C, thr, keep, x4.z, y4.z, z4.z, u4.z, v4.z, rem > 2, a);
-    accumulate_one(T, C, thr, keep, x4.w, y4.w, z4.w, u4.w, v4.w, rem > 3, a);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], rem > k, a);
   }
 
+  STAMP(4);
   float v[PICP_NPART];
 #pragma unroll
   for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
@@ -429,12 +590,21 @@ extern "C" __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
   __syncthreads();
   if (tid < PICP_NPART) {
-    float s = s_wave[0][tid];
+    float sum = s_wave[0][tid];
 #pragma unroll
-    for (int w = 1; w < PICP_BLOCK / 64; ++w) s += s_wave[w][tid];
-    part_out[(size_t)blockIdx.x * PICP_NPART + tid] = s;
+    for (int w = 1; w < PICP_BLOCK / 64; ++w) sum += s_wave[w][tid];
+    part_out[(size_t)blockIdx.x * PICP_NPART + tid] = sum;
   }
+  STAMP(5);
 }
+
+#ifdef PICP_STAMPS
+extern "C" hipError_t picp_debug_stamps(unsigned long long* out, size_t n_words) {
+  const size_t cap = sizeof(picp_stamps) / sizeof(unsigned long long);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_stamps), (n_words < cap ? n_words : cap) * 8, 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
 
 // IntPairVector gather: pairs[k] = (image idx, world idx) (src/picp_solver.cpp:65-66).
 extern "C" __global__ void picp_gather_kernel(const float* __restrict__ world,
@@ -530,15 +700,22 @@ extern "C" __global__ void picp_triangulate_kernel(const float* __restrict__ P1,
 
 // ------------------------------- host launch wrappers -------------------------------
 // (called by picp_runtime.cpp; every shape/grid assumption is checked there first)
-extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, const float* X,
+extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, const float* X,
                                         const float* Y, const float* Z, const float* U,
-                                        const float* V, const PicpProblem* probs,
-                                        const int4* blkinfo, const PicpState* st_in,
-                                        PicpState* st_out, const float* part_in,
-                                        float* part_out, int j, int finalize) {
-  if (grid <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(picp_round_kernel, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U,
-                     V, probs, blkinfo, st_in, st_out, part_in, part_out, j, finalize);
+                                        const float* V, const PicpArgs* args,
+                                        const PicpProblem* probs, const int4* blkinfo,
+                                        const PicpState* st_in, PicpState* st_out,
+                                        const float* part_in, float* part_out, int j,
+                                        int finalize) {
+  if (grid <= 0 || !args) return hipErrorInvalidValue;
+  if (vec == 4)
+    hipLaunchKernelGGL(picp_round_kernel<4>, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U,
+                       V, *args, probs, blkinfo, st_in, st_out, part_in, part_out, j, finalize);
+  else if (vec == 1)
+    hipLaunchKernelGGL(picp_round_kernel<1>, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U,
+                       V, *args, probs, blkinfo, st_in, st_out, part_in, part_out, j, finalize);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -20,12 +20,13 @@
 #include "picp_c.h"
 #include "picp_internal.h"
 
-extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, const float* X,
+extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, const float* X,
                                         const float* Y, const float* Z, const float* U,
-                                        const float* V, const PicpProblem* probs,
-                                        const int4* blkinfo, const PicpState* st_in,
-                                        PicpState* st_out, const float* part_in,
-                                        float* part_out, int j, int finalize);
+                                        const float* V, const PicpArgs* args,
+                                        const PicpProblem* probs, const int4* blkinfo,
+                                        const PicpState* st_in, PicpState* st_out,
+                                        const float* part_in, float* part_out, int j,
+                                        int finalize);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -142,8 +143,14 @@ struct picp_batch {
   PicpState* st_pinned = nullptr;  // np_cap states
   std::vector<PicpState> init_h;
   std::vector<PicpState> result_h;
-  bool probs_dirty = true;
+  bool params_set = false;
   picp_params params;
+  PicpArgs args;               // by-value kernel arguments (baked into the captured graph)
+  int ipb = PICP_BLOCK;        // items per linearize block
+  int vec = 1;                 // correspondences per lane per chunk (1 or 4)
+  int uniform = 0;             // all problems the same size -> no block tables
+  int n_u = 0;
+  int64_t stride_u = 0;
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -171,11 +178,12 @@ static int items_per_block(int64_t total) {
     int v = atoi(env);
     if (v >= 4) return (int)round_up(v, 4);
   }
-  // one float4 per lane per block for latency-bound single frames; deeper per-lane
-  // accumulation for large (HBM-streaming) batches to amortise the block reduction
+  // Latency-bound single frames: one correspondence per lane (spread over every SIMD).
+  // Large batches (HBM streaming): float4 per lane and several chunks per lane to amortise the
+  // block reduction and the partial traffic.
+  if (total <= ((int64_t)1 << 18)) return 2 * PICP_BLOCK;  // measured best for C2 (tools/sweep.py)
   if (total >= (int64_t)8 << 20) return PICP_BLOCK * 4 * 4;
-  if (total >= (int64_t)2 << 20) return PICP_BLOCK * 4 * 2;
-  return PICP_BLOCK * 4;
+  return PICP_BLOCK * 4 * 2;
 }
 
 // (Re)build the partition for correspondence offsets `offs` (np+1 entries).
@@ -187,6 +195,13 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
   b->offs.assign(offs, offs + np + 1);
   b->total = offs[np];
   const int ipb = items_per_block(b->total);
+  b->ipb = ipb;
+  b->vec = (ipb >= 4 * PICP_BLOCK) ? 4 : 1;
+  b->uniform = 1;
+  for (int i = 1; i < np; ++i)
+    if (offs[i + 1] - offs[i] != offs[1] - offs[0]) b->uniform = 0;
+  b->n_u = (int)(offs[1] - offs[0]);
+  b->stride_u = round_up(b->n_u, 4);
   b->plane_off.resize(np);
   int64_t pos = 0;
   int nblk = 0;
@@ -262,7 +277,8 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
   }
   HIP_TRY(hipMemcpyAsync(b->init_d, b->init_h.data(), (size_t)np * sizeof(PicpState), hipMemcpyHostToDevice, b->stream));
   b->result_h.assign(np, PicpState{});
-  b->probs_dirty = true;
+  HIP_TRY(hipMemcpyAsync(b->probs_d, b->probs_h.data(), (size_t)np * sizeof(PicpProblem), hipMemcpyHostToDevice, b->stream));
+  b->params_set = false;
   drop_graph(b);
   HIP_TRY(hipStreamSynchronize(b->stream));
   return PICP_OK;
@@ -272,24 +288,33 @@ static int batch_upload_params(picp_batch* b, const picp_params* prm) {
   CHECK_ARG(prm, "null params");
   CHECK_ARG(prm->max_rounds >= 0 && prm->max_rounds <= 100000, "params.max_rounds out of range");
   CHECK_ARG(!(prm->threshold != prm->threshold), "params.threshold is NaN");
-  const bool same = !b->probs_dirty && memcmp(&b->params, prm, sizeof(picp_params)) == 0;
-  if (same) return PICP_OK;
-  for (int i = 0; i < b->np; ++i) {
-    PicpProblem& P = b->probs_h[i];
-    P.rows = b->rows;
-    P.cols = b->cols;
-    memcpy(P.K, b->K, sizeof(P.K));
-    P.threshold = prm->threshold;
-    P.damping = prm->damping;
-    P.min_inliers = prm->min_inliers;
-    P.keep_outliers = prm->keep_outliers ? 1 : 0;
-    P.max_rounds = prm->max_rounds;
-    P.conv_eps = prm->conv_eps;
-  }
-  HIP_TRY(hipMemcpyAsync(b->probs_d, b->probs_h.data(), (size_t)b->np * sizeof(PicpProblem), hipMemcpyHostToDevice, b->stream));
+  if (b->params_set && memcmp(&b->params, prm, sizeof(picp_params)) == 0) return PICP_OK;
+  PicpArgs& A = b->args;
+  memset(&A, 0, sizeof(A));
+  memcpy(A.K, b->K, sizeof(A.K));
+  A.maxx = (float)(b->cols - 1);
+  A.maxy = (float)(b->rows - 1);
+  A.threshold = prm->threshold;
+  A.damping = prm->damping;
+  A.conv_eps = prm->conv_eps;
+  A.min_inliers = prm->min_inliers;
+  A.keep_outliers = prm->keep_outliers ? 1 : 0;
+  A.max_rounds = prm->max_rounds;
+  A.uniform = b->uniform;
+  A.n_u = b->n_u;
+  A.nblk_u = b->uniform ? b->nblk / b->np : 0;
+  A.ipb = b->ipb;
+  A.stride_u = b->stride_u;
   b->params = *prm;
-  b->probs_dirty = false;
+  b->params_set = true;
+  drop_graph(b);  // the arguments are baked into the captured launches
   return PICP_OK;
+}
+
+static hipError_t launch_round(picp_batch* b, int j, int fin, int in_buf) {
+  return picp_launch_round(b->stream, fin ? b->np : b->nblk, b->vec, b->X(), b->Y(), b->Z(), b->U(),
+                           b->V(), &b->args, b->probs_d, b->blk_d, b->st_d[in_buf], b->st_d[in_buf ^ 1],
+                           b->part_d[in_buf], b->part_d[in_buf ^ 1], j, fin);
 }
 
 // Enqueue the R+1 launches (plus the initial-state copy) of a fused solve on the stream.
@@ -298,11 +323,7 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
                                 hipMemcpyDeviceToDevice, b->stream);
   if (e != hipSuccess) return e;
   for (int j = 0; j <= R; ++j) {
-    const int fin = (j == R) ? 1 : 0;
-    const int grid = fin ? b->np : b->nblk;
-    e = picp_launch_round(b->stream, grid, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d,
-                          b->blk_d, b->st_d[(j + 1) & 1], b->st_d[j & 1], b->part_d[(j + 1) & 1],
-                          b->part_d[j & 1], j, fin);
+    e = launch_round(b, j, (j == R) ? 1 : 0, (j + 1) & 1);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -517,9 +538,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
       for (int j = 0; j <= R; ++j) {
         const int fin = (j == R) ? 1 : 0;
         HIP_TRY(hipEventRecord(ev[j], b->stream));
-        HIP_TRY(picp_launch_round(b->stream, fin ? b->np : b->nblk, b->X(), b->Y(), b->Z(), b->U(), b->V(),
-                                  b->probs_d, b->blk_d, b->st_d[(j + 1) & 1], b->st_d[j & 1],
-                                  b->part_d[(j + 1) & 1], b->part_d[j & 1], j, fin));
+        HIP_TRY(launch_round(b, j, fin, (j + 1) & 1));
       }
       HIP_TRY(hipEventRecord(ev[R + 1], b->stream));
       HIP_TRY(hipEventSynchronize(ev[R + 1]));
@@ -596,7 +615,7 @@ extern "C" int picp_set_camera(picp_t* h, int rows, int cols, const float K[9]) 
   h->b->rows = rows;
   h->b->cols = cols;
   memcpy(h->b->K, K, sizeof(h->b->K));
-  h->b->probs_dirty = true;
+  h->b->params_set = false;
   return PICP_OK;
 }
 
@@ -721,10 +740,8 @@ extern "C" int picp_one_round(picp_t* h, float threshold, float damping, int min
   rc = handle_upload_pose(h);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
-  HIP_TRY(picp_launch_round(b->stream, b->nblk, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d, b->blk_d,
-                            b->st_d[1], b->st_d[0], b->part_d[1], b->part_d[0], 0, 0));
-  HIP_TRY(picp_launch_round(b->stream, 1, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d, b->blk_d,
-                            b->st_d[0], b->st_d[1], b->part_d[0], b->part_d[1], 1, 1));
+  HIP_TRY(launch_round(b, 0, 0, 1));
+  HIP_TRY(launch_round(b, 1, 1, 0));
   b->last_rounds = 1;
   rc = batch_read_results(b);
   if (rc) return rc;
@@ -769,8 +786,7 @@ extern "C" int picp_linearize(picp_t* h, float threshold, int keep_outliers, dou
   rc = handle_upload_pose(h);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
-  HIP_TRY(picp_launch_round(b->stream, b->nblk, b->X(), b->Y(), b->Z(), b->U(), b->V(), b->probs_d, b->blk_d,
-                            b->st_d[1], b->st_d[0], b->part_d[1], b->part_d[0], 0, 0));
+  HIP_TRY(launch_round(b, 0, 0, 1));
   std::vector<float> part((size_t)b->nblk * PICP_NPART);
   HIP_TRY(hipMemcpyAsync(part.data(), b->part_d[0], part.size() * sizeof(float), hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));

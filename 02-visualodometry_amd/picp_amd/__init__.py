@@ -18,7 +18,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpicp_amd.so")
+# PICP_LIB selects a diagnostic build (tools/stamps.py); the default is the shipped library
+LIB_PATH = os.environ.get("PICP_LIB") or os.path.join(PKG_ROOT, "lib", "libpicp_amd.so")
 
 OK = 0
 ERR_ARG = -1

@@ -109,7 +109,8 @@ def test_solve_matches_oracle(native, oracle, n, seed, of, keep):
     assert synth.se3_log_norm(s.pose(), T_ref) < POSE_TOL
     assert synth.se3_log_norm(s.pose(), T_f) < POSE_TOL
     assert abs(st["n_in"] - st_ref["n_in"]) <= max(2, n // 10000)
-    assert synth.se3_log_norm(s.pose(), p["T_gt"]) < 1e-2
+    if not keep:  # keep_outliers=True: the saturated outliers still pull (biased, as in the reference)
+        assert synth.se3_log_norm(s.pose(), p["T_gt"]) < 1e-2
 
 
 def test_solve_convergence_rule_matches_oracle(native, oracle):
