@@ -1,0 +1,328 @@
+// picp_device.h -- device-side math shared by the PICP kernels (picp_kernels.hip, multi-launch
+// rounds; picp_persistent.hip, single-launch rounds): per-correspondence projection/Jacobian/gate
+// (src/camera.h:24-36, src/picp_solver.cpp:26-91), the wave64 normal-equation reduction, the
+// damped 6x6 LDL^T solve and the v2tEuler left update (src/picp_solver.cpp:93-105,
+// src/defs.h:100-136), and the icp_test convergence rule (exec/icp_test.cpp:99-106).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <stdint.h>
+
+#include "picp_internal.h"
+
+namespace picp {
+
+struct Pose {
+  float r00, r01, r02, r10, r11, r12, r20, r21, r22;
+  float t0, t1, t2;
+};
+
+struct Cam {
+  float k00, k01, k02, k10, k11, k12, k20, k21, k22;
+  float maxx, maxy;  // cols-1, rows-1 (src/camera.h:31,33)
+};
+
+struct Acc {
+  float h[21];  // upper triangle of H, row-major (i<=j)
+  float b[6];
+  float chi_in, chi_out, n_in, n_proj;
+};
+
+// ---------------------------------------------------------------------------------------
+// Per-correspondence math.  The block that decides projectability and the chi2 gate is
+// compiled with FP contraction OFF and evaluates every sum left to right, exactly like the
+// CPU oracle (oracle/picp_oracle.c), so inlier/outlier/skip decisions are bit-identical to
+// the oracle at the same pose.  The Jacobian and accumulation are free to use FMA.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, float thr,
+                                               bool keep, float x, float y, float z, float u,
+                                               float v, bool in_range, Acc& a) {
+  float pc0, pc1, pc2, ph0, ph1, ph2, iz, e0, e1, chi;
+  bool valid;
+  {
+#pragma clang fp contract(off)
+    // src/camera.h:26  pc = R*p + t
+    pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;
+    pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
+    pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
+    // src/camera.h:29  ph = K*pc
+    ph0 = (C.k00 * pc0 + C.k01 * pc1) + C.k02 * pc2;
+    ph1 = (C.k10 * pc0 + C.k11 * pc1) + C.k12 * pc2;
+    ph2 = (C.k20 * pc0 + C.k21 * pc1) + C.k22 * pc2;
+    // src/camera.h:30 / picp_solver.cpp:44: (float)(1.0/(double)z) == correctly rounded
+    // 1.0f/z (double rounding is innocuous for division at 53 >= 2*24+2); hipcc's default
+    // fp32 division is correctly rounded.
+    iz = 1.0f / ph2;
+    const float ix = ph0 * iz;
+    const float iy = ph1 * iz;
+    // src/camera.h:27-28 (z<=0 rejects; NaN passes as in the reference) and :31-34
+    valid = in_range && !(pc2 <= 0.0f) &&
+            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    e0 = ix - u;  // src/picp_solver.cpp:34
+    e1 = iy - v;
+    chi = e0 * e0 + e1 * e1;  // src/picp_solver.cpp:74
+  }
+  // src/picp_solver.cpp:75-89: strict gate, sqrt kernel weight, outliers only with keep
+  const bool outlier = chi > thr;
+  const bool inl = valid && !outlier;
+  const bool use = inl || (valid && keep);
+  const float lambda = outlier ? sqrtf(thr / chi) : 1.0f;
+  const float w = inl ? 1.0f : lambda;
+  a.chi_in += inl ? chi : 0.0f;
+  a.chi_out += (valid && outlier) ? chi : 0.0f;
+  a.n_in += inl ? 1.0f : 0.0f;
+  a.n_proj += valid ? 1.0f : 0.0f;
+  // unused terms are zeroed by select before the Jacobian, so a skipped point (possibly
+  // with an infinite iz) can never inject inf/NaN into H or b
+  iz = use ? iz : 0.0f;
+  pc0 = use ? pc0 : 0.0f;
+  pc1 = use ? pc1 : 0.0f;
+  pc2 = use ? pc2 : 0.0f;
+  ph0 = use ? ph0 : 0.0f;
+  ph1 = use ? ph1 : 0.0f;
+  e0 = use ? e0 : 0.0f;
+  e1 = use ? e1 : 0.0f;
+  // src/picp_solver.cpp:38-52: J = Jp * K * [I | skew(-pc)]
+  const float iz2 = iz * iz;
+  const float jp02 = -ph0 * iz2, jp12 = -ph1 * iz2;
+  const float a00 = iz * C.k00 + jp02 * C.k20;  // (Jp*K)(0,c)
+  const float a01 = iz * C.k01 + jp02 * C.k21;
+  const float a02 = iz * C.k02 + jp02 * C.k22;
+  const float a10 = iz * C.k10 + jp12 * C.k20;  // (Jp*K)(1,c)
+  const float a11 = iz * C.k11 + jp12 * C.k21;
+  const float a12 = iz * C.k12 + jp12 * C.k22;
+  float J0[6], J1[6];
+  J0[0] = a00; J0[1] = a01; J0[2] = a02;
+  J0[3] = a02 * pc1 - a01 * pc2;
+  J0[4] = a00 * pc2 - a02 * pc0;
+  J0[5] = a01 * pc0 - a00 * pc1;
+  J1[0] = a10; J1[1] = a11; J1[2] = a12;
+  J1[3] = a12 * pc1 - a11 * pc2;
+  J1[4] = a10 * pc2 - a12 * pc0;
+  J1[5] = a11 * pc0 - a10 * pc1;
+  float W0[6], W1[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    W0[i] = w * J0[i];
+    W1[i] = w * J1[i];
+  }
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      a.h[k] = fmaf(W0[i], J0[j], fmaf(W1[i], J1[j], a.h[k]));
+      ++k;
+    }
+    a.b[i] = fmaf(W0[i], e0, fmaf(W1[i], e1, a.b[i]));
+  }
+}
+
+// Cross-lane moves without the LDS crossbar.  gfx950 v_permlane32_swap / v_permlane16_swap
+// exchange half-waves / odd-even 16-lane rows between two registers; DPP reads a partner
+// lane inside a 16-lane row (row_mirror l^15, row_half_mirror l^7, quad_perm l^2, l^1).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+#define DPP_ROW_MIRROR 0x140
+#define DPP_ROW_HALF_MIRROR 0x141
+#define DPP_QUAD_XOR2 0x4E  // quad_perm [2,3,0,1]
+#define DPP_QUAD_XOR1 0xB1  // quad_perm [1,0,3,2]
+
+// Halving-butterfly step inside a 16-lane row: lanes l and P(l) (P an involution that flips
+// bit HB) exchange the half of the 2*HALF values the other keeps.
+template <int CTRL, int HB, int HALF>
+__device__ __forceinline__ void bfly_dpp(float* v, int lane) {
+  const bool hi = (lane >> HB) & 1;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const float send = hi ? v[i] : v[i + HALF];
+    const float keep = hi ? v[i + HALF] : v[i];
+    v[i] = keep + dpp<CTRL>(send);
+  }
+}
+
+// Sum 32 per-lane values over the 64 lanes of a wave (32 -> 16 -> 8 -> 4 -> 2 -> 1 values per
+// lane).  The swap steps need no select: after v_permlane32_swap(a=v[i], b=v[i+16]) the low
+// half holds (own v[i], partner v[i]) and the high half (partner v[i+16], own v[i+16]), so a+b
+// is the pair sum of the half each lane keeps.  Returns, in every lane, the wave total of value
+// index (lane >> 1).
+__device__ __forceinline__ float wave_reduce32(float* v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 16]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  bfly_dpp<DPP_ROW_MIRROR, 3, 4>(v, lane);
+  bfly_dpp<DPP_ROW_HALF_MIRROR, 2, 2>(v, lane);
+  bfly_dpp<DPP_QUAD_XOR2, 1, 1>(v, lane);
+  return v[0] + dpp<DPP_QUAD_XOR1>(v[0]);
+}
+
+// 1/d in float: hardware v_rcp_f32 estimate refined by one Newton step (<= 1 ulp for normal
+// d); |d| <= FLT_MIN -> 0 (Eigen's LDLT zero-pivot rule for float, src/picp_solver.cpp:102).
+__device__ __forceinline__ float rcp32(float d) {
+  float r = __builtin_amdgcn_rcpf(d);
+  r = fmaf(r, fmaf(-d, r, 1.0f), r);
+  return (fabsf(d) > FLT_MIN) ? r : 0.0f;
+}
+
+// Damped normal equations -> dx.  float32 LDL^T, the precision the reference solves in
+// (Matrix6f::ldlt, src/picp_solver.cpp:102); H and b arrive as exact double sums.  Plain LDL^T
+// without Eigen's diagonal pivoting (H + damping*I is SPD: pivoting only changes rounding).
+// Fully unrolled: registers only, one lane.
+__device__ __forceinline__ void ldlt6_solve(float A[6][6], const float rhs[6], float x[6]) {
+  float L[6][6], D[6], iD[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float d = A[j][j];
+    float LD[6];
+#pragma unroll
+    for (int k = 0; k < j; ++k) {
+      LD[k] = L[j][k] * D[k];
+      d = fmaf(-LD[k], L[j][k], d);
+    }
+    D[j] = d;
+    iD[j] = rcp32(d);
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      float s = A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) s = fmaf(-L[i][k], LD[k], s);
+      L[i][j] = s * iD[j];
+    }
+  }
+  float y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = rhs[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s = fmaf(-L[i][k], y[k], s);
+    y[i] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) y[i] *= iD[i];
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s = fmaf(-L[k][i], x[k], s);
+    x[i] = s;
+  }
+}
+
+// sin/cos of a GN increment angle.  Increments are small, so the float Taylor series (exact to
+// float rounding for |a| <= 1/16: next term a^9/9! < 1e-16) avoids sincosf's range reduction
+// on the single-lane critical path; larger angles take the libm path.
+__device__ __forceinline__ void small_sincos(float a, float* s, float* c) {
+  if (fabsf(a) <= 0.0625f) {
+    const float a2 = a * a;
+    *s = a * fmaf(a2, fmaf(a2, fmaf(a2, -1.0f / 5040.0f, 1.0f / 120.0f), -1.0f / 6.0f), 1.0f);
+    *c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 1.0f / 40320.0f, -1.0f / 720.0f), 1.0f / 24.0f), -0.5f), 1.0f);
+  } else {
+    sincosf(a, s, c);
+  }
+}
+
+// src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
+// src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
+__device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
+  float sa, ca, sb, cb, sc, cc;
+  small_sincos(dx[3], &sa, &ca);
+  small_sincos(dx[4], &sb, &cb);
+  small_sincos(dx[5], &sc, &cc);
+  const float Rx[3][3] = {{1.f, 0.f, 0.f}, {0.f, ca, -sa}, {0.f, sa, ca}};
+  const float Ry[3][3] = {{cb, 0.f, sb}, {0.f, 1.f, 0.f}, {-sb, 0.f, cb}};
+  const float Rz[3][3] = {{cc, -sc, 0.f}, {sc, cc, 0.f}, {0.f, 0.f, 1.f}};
+  float Rxy[3][3], Rd[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float s = Rx[i][0] * Ry[0][j];
+      s = s + Rx[i][1] * Ry[1][j];
+      s = s + Rx[i][2] * Ry[2][j];
+      Rxy[i][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float s = Rxy[i][0] * Rz[0][j];
+      s = s + Rxy[i][1] * Rz[1][j];
+      s = s + Rxy[i][2] * Rz[2][j];
+      Rd[i][j] = s;
+    }
+  float Rn[9], tn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float s = Rd[i][0] * R[j * 3 + 0];
+      s = s + Rd[i][1] * R[j * 3 + 1];
+      s = s + Rd[i][2] * R[j * 3 + 2];
+      Rn[j * 3 + i] = s;
+    }
+    float s = Rd[i][0] * t[0];
+    s = s + Rd[i][1] * t[1];
+    s = s + Rd[i][2] * t[2];
+    tn[i] = s + dx[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = tn[i];
+}
+
+// Finish round (j-1) of a problem from its block-partial totals: H, b, stats -> new state.
+// Runs in one lane; everything is indexed by compile-time constants.
+__device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState& s,
+                                             const double* tot, int j, PicpState& ns) {
+  ns = s;
+  ns.chi_in = (float)tot[PICP_P_CHI_IN];
+  ns.chi_out = (float)tot[PICP_P_CHI_OUT];
+  ns.n_in = (int32_t)tot[PICP_P_N_IN];
+  ns.n_proj = (int32_t)tot[PICP_P_N_PROJ];
+  ns.rounds = j;
+  float H[6][6];
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = r; c < 6; ++c) {
+      const double h = tot[PICP_P_H + k] + ((r == c) ? (double)A.damping : 0.0);  // :96
+      H[r][c] = (float)h;
+      H[c][r] = (float)h;
+      ++k;
+    }
+  if (ns.n_in < A.min_inliers) {  // src/picp_solver.cpp:97-100
+    ns.ok = 0;
+    ns.done = 1;
+    return;
+  }
+  float nb[6], dx[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) nb[r] = (float)(-tot[PICP_P_B + r]);
+  ldlt6_solve(H, nb, dx);        // :102
+  apply_update(dx, ns.R, ns.t);  // :103
+  ns.ok = 1;
+  // exec/icp_test.cpp:99-106
+  const float prev = s.chi_prev, cur = ns.chi_in;
+  const float rel = (prev > 1e-10f) ? fabsf(prev - cur) / prev : 0.0f;
+  if (rel < A.conv_eps) {
+    ns.converged = 1;
+    ns.done = 1;
+  } else {
+    ns.chi_prev = cur;
+  }
+  if (j >= A.max_rounds) ns.done = 1;
+}
+
+}  // namespace picp

@@ -1,0 +1,278 @@
+// picp_persistent.hip -- the whole exec/icp_test.cpp:88-107 loop in ONE launch, for batches whose
+// blocks all fit on the chip at once (a single 100k-1M frame, a few frames).
+//
+// Why: with one launch per round the critical path of a round is launch gap + a chip-wide
+// re-read of every block partial + the serial solve (tools/stamps.py).  Here each
+// block loads its slice of the frame into REGISTERS once (never re-read from HBM), and each
+// round costs one fan-in and one fan-out inside the launch:
+//   1. every block linearizes its slice at the current pose and publishes its 32-float partial
+//      as 32 granules {tag = round+1, value} (8-byte relaxed agent-scope atomic stores: the R2
+//      hand-off of cdna_hip_programming.md Guideline 16 -- the data IS the flag, no fences);
+//   2. the problem's leader block (its first block) sweeps those granules until every tag
+//      matches, sums them in a FIXED order (deterministic), solves the damped 6x6 system and
+//      applies the update (picp_device.h: finish_round), then publishes the new pose as 16
+//      granules {round+1, word};
+//   3. every other block polls the 16 pose granules (one wave), then starts the next round.
+// Correctness does not depend on placement or timing: only tags are trusted.  Blocks must be
+// co-resident (the host caps the grid at the CU count with ~110 VGPRs / 10 KB LDS per block),
+// every spin is bounded by an s_memrealtime deadline (timeout -> error word, loop exits), and
+// the host zeroes every granule with a memset node before each launch.
+#include "picp_device.h"
+
+using namespace picp;
+
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+#define PICP_MAX_PBLK 256   // max blocks per problem in this mode (sweep registers)
+#define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
+
+// Diagnostic build only (-DPICP_STAMPS): s_memrealtime per phase of rounds (epochs) 11 and 12.
+#ifdef PICP_STAMPS
+__device__ unsigned long long picp_pstamps[2][256][8];
+#define PSTAMP(k)                                                                              \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && (epoch == 11 || epoch == 12) && blockIdx.x < 256)                  \
+      picp_pstamps[epoch - 11][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+extern "C" hipError_t picp_debug_pstamps(unsigned long long* out, size_t n_words);
+#else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+__device__ __forceinline__ unsigned long long granule(unsigned epoch, float v) {
+  return ((unsigned long long)epoch << 32) | (unsigned long long)__float_as_uint(v);
+}
+
+__device__ __forceinline__ bool timed_out(unsigned long long deadline) {
+  return __builtin_amdgcn_s_memrealtime() > deadline;
+}
+
+template <int NPT>
+__global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
+    const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+    const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
+    const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
+    unsigned long long* gpart, unsigned long long* gpose, unsigned int* err,
+    unsigned long long timeout_ticks) {
+  __shared__ double s_red[8][PICP_NPART + 1];
+  __shared__ double s_tot[PICP_NPART];
+  __shared__ float s_wave[PICP_BLOCK / 64][PICP_NPART];
+  __shared__ float s_pose[12];
+  __shared__ int s_done;
+  __shared__ PicpState s_st;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nblk = A.nblk_u;
+  const int p = (int)blockIdx.x / nblk;
+  const int kb = (int)blockIdx.x - p * nblk;
+  const int first = kb * A.ipb;
+  const int count = max(0, min(A.ipb, A.n_u - first));
+  const int64_t base = (int64_t)p * A.stride_u + first;
+  const bool leader = (kb == 0);
+  gu64_t* my_part = ((gu64_t*)gpart) + (size_t)blockIdx.x * PICP_NPART;
+  gu64_t* prob_part = ((gu64_t*)gpart) + (size_t)p * nblk * PICP_NPART;
+  gu64_t* prob_pose = ((gu64_t*)gpose) + (size_t)p * PICP_POSE_GRAN;
+  gu32_t* errw = ((gu32_t*)err);
+
+  // this block's slice, loaded once into registers (coalesced: item = tid + k*BLOCK)
+  float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int i = tid + k * PICP_BLOCK;
+    const int ic = min(i, max(count - 1, 0));
+    xs[k] = X[base + ic];
+    ys[k] = Y[base + ic];
+    zs[k] = Z[base + ic];
+    us[k] = U[base + ic];
+    vs[k] = V[base + ic];
+  }
+
+  if (tid == 0) {  // initial state, as launch 0 of the multi-launch path
+    PicpState s = st_in[p];
+    s.chi_prev = FLT_MAX;  // exec/icp_test.cpp:89
+    s.chi_in = s.chi_out = 0.0f;
+    s.n_in = s.n_proj = 0;
+    s.rounds = 0;
+    s.done = (A.max_rounds <= 0) ? 1 : 0;
+    s.ok = 1;
+    s.converged = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s_pose[i] = s.R[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
+    s_done = s.done;
+    if (leader) {
+      s_st = s;
+      if (s.done) st_out[p] = s;
+    }
+  }
+  __syncthreads();
+  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
+
+  Cam C;
+  C.k00 = A.K[0]; C.k10 = A.K[1]; C.k20 = A.K[2];
+  C.k01 = A.K[3]; C.k11 = A.K[4]; C.k21 = A.K[5];
+  C.k02 = A.K[6]; C.k12 = A.K[7]; C.k22 = A.K[8];
+  C.maxx = A.maxx;
+  C.maxy = A.maxy;
+  const float thr = A.threshold;
+  const bool keep = A.keep_outliers != 0;
+
+  for (unsigned epoch = 1; !s_done; ++epoch) {
+    // ---- 1. linearize the slice at the current pose, publish the block partial ----
+    PSTAMP(0);
+    Pose T;
+    T.r00 = s_pose[0]; T.r10 = s_pose[1]; T.r20 = s_pose[2];
+    T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
+    T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
+    T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
+    Acc a;
+#pragma unroll
+    for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
+    a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], tid + k * PICP_BLOCK < count, a);
+    float v[PICP_NPART];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
+    v[PICP_P_CHI_IN] = a.chi_in;
+    v[PICP_P_CHI_OUT] = a.chi_out;
+    v[PICP_P_N_IN] = a.n_in;
+    v[PICP_P_N_PROJ] = a.n_proj;
+    v[31] = 0.0f;
+    const float wsum = wave_reduce32(v, lane);
+    if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
+    __syncthreads();
+    if (tid < PICP_NPART) {
+      float sum = s_wave[0][tid];
+#pragma unroll
+      for (int w = 1; w < PICP_BLOCK / 64; ++w) sum += s_wave[w][tid];
+      __hip_atomic_store(my_part + tid, granule(epoch, sum), RLX_AGENT);
+    }
+    PSTAMP(1);
+
+    if (leader) {
+      // ---- 2. sweep the problem's partials (entry e = tid&31 of blocks (tid>>5) + 8i) ----
+      const int e = tid & 31, g = tid >> 5;
+      constexpr int MAXG = PICP_MAX_PBLK / (PICP_BLOCK / 32);
+      unsigned long long gv[MAXG];
+      bool ok = false;
+      for (;;) {
+        ok = true;
+#pragma unroll
+        for (int i = 0; i < MAXG; ++i) {
+          const int b = g + 8 * i;
+          gv[i] = __hip_atomic_load(prob_part + (size_t)min(b, nblk - 1) * PICP_NPART + e, RLX_AGENT);
+          ok &= (b >= nblk) || ((unsigned)(gv[i] >> 32) == epoch);
+        }
+        if (ok) break;
+        if (timed_out(deadline)) {
+          __hip_atomic_store(errw, 1u, RLX_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < MAXG; ++i)
+        if (g + 8 * i < nblk) acc += (double)__uint_as_float((unsigned)gv[i]);
+      s_red[g][e] = acc;
+      __syncthreads();
+      PSTAMP(2);
+      if (tid < PICP_NPART) {
+        double t = 0.0;
+#pragma unroll
+        for (int gg = 0; gg < PICP_BLOCK / 32; ++gg) t += s_red[gg][tid];
+        s_tot[tid] = t;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double tot[PICP_NPART];
+#pragma unroll
+        for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
+        PicpState ns;
+        PSTAMP(4);
+        finish_round(A, s_st, tot, (int)epoch, ns);
+        PSTAMP(5);
+        if (__hip_atomic_load(errw, RLX_AGENT) != 0u) ns.done = 1;  // a sweep timed out
+        s_st = ns;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
+        s_done = ns.done;
+        if (ns.done) st_out[p] = ns;
+      }
+      __syncthreads();
+      PSTAMP(3);
+      // ---- publish the new pose (and the done flag) ----
+      if (tid < PICP_POSE_GRAN) {
+        const float w = (tid < 12) ? s_pose[tid] : ((tid == 12) ? __int_as_float(s_done) : 0.0f);
+        __hip_atomic_store(prob_pose + tid, granule(epoch, w), RLX_AGENT);
+      }
+    } else {
+      // ---- 3. wait for the leader's pose of this round (one wave, 16 lanes) ----
+      if (wave == 0) {
+        unsigned long long gp = 0;
+        for (;;) {
+          bool ok = true;
+          if (lane < PICP_POSE_GRAN) {
+            gp = __hip_atomic_load(prob_pose + lane, RLX_AGENT);
+            ok = (unsigned)(gp >> 32) == epoch;
+          }
+          if (__all(ok)) break;
+          if (timed_out(deadline)) {
+            if (lane == 0) __hip_atomic_store(errw, 2u, RLX_AGENT);
+            gp = ((unsigned long long)epoch << 32) | (lane == 12 ? 1u : 0u);  // force done
+            if (lane < 12) gp = ((unsigned long long)epoch << 32) | __float_as_uint(s_pose[lane]);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane < 12) s_pose[lane] = __uint_as_float((unsigned)gp);
+        if (lane == 12) s_done = (int)(unsigned)gp;
+      }
+      __syncthreads();
+      PSTAMP(2);
+    }
+  }
+}
+
+#ifdef PICP_STAMPS
+extern "C" hipError_t picp_debug_pstamps(unsigned long long* out, size_t n_words) {
+  const size_t cap = sizeof(picp_pstamps) / sizeof(unsigned long long);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_pstamps), (n_words < cap ? n_words : cap) * 8, 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
+
+// ------------------------------- host launch wrapper -------------------------------
+extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int npt, const float* X,
+                                             const float* Y, const float* Z, const float* U,
+                                             const float* V, const PicpArgs* args,
+                                             const PicpState* st_in, PicpState* st_out,
+                                             unsigned long long* gpart, unsigned long long* gpose,
+                                             unsigned int* err, unsigned long long timeout_ticks) {
+  if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
+#define PICP_LAUNCH_P(N)                                                                              \
+  hipLaunchKernelGGL(picp_persistent_kernel<N>, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U, \
+                     V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks)
+  switch (npt) {
+    case 1: PICP_LAUNCH_P(1); break;
+    case 2: PICP_LAUNCH_P(2); break;
+    case 4: PICP_LAUNCH_P(4); break;
+    case 8: PICP_LAUNCH_P(8); break;
+    case 16: PICP_LAUNCH_P(16); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef PICP_LAUNCH_P
+  return hipGetLastError();
+}

@@ -27,6 +27,12 @@ extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, c
                                         const PicpState* st_in, PicpState* st_out,
                                         const float* part_in, float* part_out, int j,
                                         int finalize);
+extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int npt, const float* X,
+                                             const float* Y, const float* Z, const float* U,
+                                             const float* V, const PicpArgs* args,
+                                             const PicpState* st_in, PicpState* st_out,
+                                             unsigned long long* gpart, unsigned long long* gpose,
+                                             unsigned int* err, unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -115,6 +121,11 @@ static void state_to_stats(const PicpState& s, picp_stats& st) {
 
 static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+#define PICP_MODE_GRAPH 0
+#define PICP_MODE_PERSISTENT 1
+#define PICP_POSE_GRAN 16
+#define PICP_MAX_PBLK 256
+
 // ------------------------------------------------------------------------------------
 // batch
 // ------------------------------------------------------------------------------------
@@ -151,6 +162,14 @@ struct picp_batch {
   int uniform = 0;             // all problems the same size -> no block tables
   int n_u = 0;
   int64_t stride_u = 0;
+  int num_cu = 256;            // compute units of the device
+  int mode = PICP_MODE_GRAPH;  // PICP_MODE_GRAPH (launch per round) / PICP_MODE_PERSISTENT
+  int npt = 1;                 // persistent: correspondences per lane held in registers
+  unsigned char* sync = nullptr;   // persistent: [err 16 B | pose granules | partial granules]
+  size_t sync_bytes = 0, sync_cap = 0;
+  int result_idx = 0;          // st_d[] holding the final state of the last solve
+  bool last_persistent = false;  // the last solve was a persistent launch (check its error word)
+  unsigned long long timeout_ticks = 20000000ull;  // 200 ms of s_memrealtime (100 MHz)
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -194,14 +213,34 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
   b->np = np;
   b->offs.assign(offs, offs + np + 1);
   b->total = offs[np];
-  const int ipb = items_per_block(b->total);
-  b->ipb = ipb;
-  b->vec = (ipb >= 4 * PICP_BLOCK) ? 4 : 1;
   b->uniform = 1;
   for (int i = 1; i < np; ++i)
     if (offs[i + 1] - offs[i] != offs[1] - offs[0]) b->uniform = 0;
   b->n_u = (int)(offs[1] - offs[0]);
   b->stride_u = round_up(b->n_u, 4);
+  // Persistent single launch when every block of the batch can be resident at once (one block
+  // per CU, each lane holding <= 16 correspondences in registers); otherwise a launch per round.
+  int ipb = items_per_block(b->total);
+  b->mode = PICP_MODE_GRAPH;
+  {
+    const char* m = getenv("PICP_MODE");
+    const bool allow = !(m && strcmp(m, "graph") == 0);
+    int bpp = b->num_cu / np;  // blocks per problem available
+    if (const char* e = getenv("PICP_PERSIST_BLOCKS")) bpp = std::max(1, std::min(bpp, atoi(e)));
+    if (allow && b->uniform && bpp >= 1) {
+      const int64_t per_block = std::max<int64_t>(1, (b->n_u + bpp - 1) / bpp);
+      int npt = 1;
+      while ((int64_t)npt * PICP_BLOCK < per_block && npt < 32) npt *= 2;
+      const int nb = (int)std::max<int64_t>(1, (b->n_u + (int64_t)npt * PICP_BLOCK - 1) / ((int64_t)npt * PICP_BLOCK));
+      if (npt <= 16 && nb <= PICP_MAX_PBLK && (int64_t)nb * np <= b->num_cu) {
+        b->mode = PICP_MODE_PERSISTENT;
+        b->npt = npt;
+        ipb = npt * PICP_BLOCK;
+      }
+    }
+  }
+  b->ipb = ipb;
+  b->vec = (ipb >= 4 * PICP_BLOCK && b->mode == PICP_MODE_GRAPH) ? 4 : 1;
   b->plane_off.resize(np);
   int64_t pos = 0;
   int nblk = 0;
@@ -247,6 +286,15 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     }
     HIP_TRY(hipHostMalloc((void**)&b->st_pinned, (size_t)np * sizeof(PicpState), hipHostMallocDefault));
     b->np_cap = np;
+  }
+  if (b->mode == PICP_MODE_PERSISTENT) {
+    b->sync_bytes = (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + (int64_t)nblk * PICP_NPART * 8, 256);
+    if (b->sync_bytes > b->sync_cap) {
+      if (b->sync) hipFree(b->sync);
+      b->sync = nullptr;
+      HIP_TRY(hipMalloc(&b->sync, b->sync_bytes));
+      b->sync_cap = b->sync_bytes;
+    }
   }
   // block table
   b->blk_h.resize(nblk);
@@ -319,6 +367,16 @@ static hipError_t launch_round(picp_batch* b, int j, int fin, int in_buf) {
 
 // Enqueue the R+1 launches (plus the initial-state copy) of a fused solve on the stream.
 static hipError_t enqueue_solve(picp_batch* b, int R) {
+  if (b->mode == PICP_MODE_PERSISTENT) {
+    // every polled word (error word and all granules) is zeroed before each launch
+    hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
+    if (e != hipSuccess) return e;
+    unsigned int* err = reinterpret_cast<unsigned int*>(b->sync);
+    unsigned long long* gpose = reinterpret_cast<unsigned long long*>(b->sync + 16);
+    unsigned long long* gpart = gpose + (size_t)b->np * PICP_POSE_GRAN;
+    return picp_launch_persistent(b->stream, b->nblk, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(),
+                                  &b->args, b->init_d, b->st_d[0], gpart, gpose, err, b->timeout_ticks);
+  }
   hipError_t e = hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState),
                                 hipMemcpyDeviceToDevice, b->stream);
   if (e != hipSuccess) return e;
@@ -353,15 +411,20 @@ static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   if (rc) return rc;
   HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
   b->last_rounds = R;
+  b->result_idx = (b->mode == PICP_MODE_PERSISTENT) ? 0 : (R & 1);
+  b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
   return PICP_OK;
 }
 
 static int batch_read_results(picp_batch* b) {
-  const int R = b->last_rounds;
-  HIP_TRY(hipMemcpyAsync(b->st_pinned, b->st_d[R & 1], (size_t)b->np * sizeof(PicpState),
+  HIP_TRY(hipMemcpyAsync(b->st_pinned, b->st_d[b->result_idx], (size_t)b->np * sizeof(PicpState),
                          hipMemcpyDeviceToHost, b->stream));
+  unsigned int err = 0;
+  if (b->last_persistent && b->sync)
+    HIP_TRY(hipMemcpyAsync(&err, b->sync, sizeof(err), hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   memcpy(b->result_h.data(), b->st_pinned, (size_t)b->np * sizeof(PicpState));
+  if (err) return set_err(PICP_ERR_DEVICE, "persistent solve: a hand-off wait timed out (code %u)", err);
   return PICP_OK;
 }
 
@@ -379,7 +442,9 @@ static int batch_create(picp_batch** out, int device, int np, const int64_t* off
   memcpy(b->K, K, sizeof(b->K));
   picp_params_default(&b->params);
   hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&b->num_cu, hipDeviceAttributeMultiprocessorCount, device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+  if (const char* t = getenv("PICP_TIMEOUT_MS")) b->timeout_ticks = (unsigned long long)(atof(t) * 1e5);
   if (e != hipSuccess) {
     delete b;
     return set_err(PICP_ERR_DEVICE, "stream create: %s", hipGetErrorString(e));
@@ -413,6 +478,7 @@ extern "C" int picp_batch_destroy(picp_batch_t* b) {
     if (b->part_d[k]) hipFree(b->part_d[k]);
   }
   if (b->st_pinned) hipHostFree(b->st_pinned);
+  if (b->sync) hipFree(b->sync);
   if (b->stream) hipStreamDestroy(b->stream);
   delete b;
   return PICP_OK;
@@ -499,10 +565,11 @@ extern "C" int picp_batch_solve(picp_batch_t* b, const picp_params* prm) {
   return batch_read_results(b);
 }
 
-extern "C" int picp_batch_info(picp_batch_t* b, int64_t* total, int* nblk) {
+extern "C" int picp_batch_info(picp_batch_t* b, int64_t* total, int* nblk, int* mode) {
   CHECK_ARG(b, "picp_batch_info: null batch");
   if (total) *total = b->total;
   if (nblk) *nblk = b->nblk;
+  if (mode) *mode = b->mode;
   return PICP_OK;
 }
 
@@ -526,32 +593,55 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
   HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
   if (total_ms) *total_ms = ms;
   b->last_rounds = R;
+  b->result_idx = (b->mode == PICP_MODE_PERSISTENT) ? 0 : (R & 1);
+  b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
   if (kernel_us) {
-    // instrumented pass: an event pair around every launch of the same solve
+    // [0]: mean launch period of the round kernel inside the replayed graphs (event time over
+    //      the timed replays / kernel launches; the graphs are back-to-back launches, so this is
+    //      the per-launch duration a kernel trace reports);
+    // [1]: mean of event pairs around single launches of the same solve (an upper bound: it
+    //      adds the event overhead to every launch).
+    const int launches = (b->mode == PICP_MODE_PERSISTENT) ? 1 : (R + 1);
+    kernel_us[0] = 1000.0f * ms / (float)(reps * launches);
+    if (b->mode == PICP_MODE_PERSISTENT) {
+      hipEvent_t a0, a1;
+      HIP_TRY(hipEventCreate(&a0));
+      HIP_TRY(hipEventCreate(&a1));
+      HIP_TRY(hipEventRecord(a0, b->stream));
+      HIP_TRY(enqueue_solve(b, R));
+      HIP_TRY(hipEventRecord(a1, b->stream));
+      HIP_TRY(hipEventSynchronize(a1));
+      float t = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&t, a0, a1));
+      kernel_us[1] = 1000.0f * t;
+      hipEventDestroy(a0);
+      hipEventDestroy(a1);
+      hipEventDestroy(e0);
+      hipEventDestroy(e1);
+      b->result_idx = 0;
+      return batch_read_results(b);
+    }
     std::vector<hipEvent_t> ev((size_t)(R + 2));
     for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
-    double lin_us = 0.0, fin_us = 0.0;
-    int lin_n = 0, fin_n = 0;
-    const int ireps = std::max(1, std::min(reps, 5));
-    for (int r = 0; r < ireps; ++r) {
-      HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
-      for (int j = 0; j <= R; ++j) {
-        const int fin = (j == R) ? 1 : 0;
-        HIP_TRY(hipEventRecord(ev[j], b->stream));
-        HIP_TRY(launch_round(b, j, fin, (j + 1) & 1));
-      }
-      HIP_TRY(hipEventRecord(ev[R + 1], b->stream));
-      HIP_TRY(hipEventSynchronize(ev[R + 1]));
-      for (int j = 0; j <= R; ++j) {
-        float t = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&t, ev[j], ev[j + 1]));
-        if (j == R) { fin_us += 1000.0 * t; ++fin_n; }
-        else { lin_us += 1000.0 * t; ++lin_n; }
-      }
+    double lin_us = 0.0;
+    int lin_n = 0;
+    HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
+    for (int j = 0; j <= R; ++j) {
+      HIP_TRY(hipEventRecord(ev[j], b->stream));
+      HIP_TRY(launch_round(b, j, (j == R) ? 1 : 0, (j + 1) & 1));
+    }
+    HIP_TRY(hipEventRecord(ev[R + 1], b->stream));
+    HIP_TRY(hipEventSynchronize(ev[R + 1]));
+    for (int j = 0; j < R; ++j) {
+      float t = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&t, ev[j], ev[j + 1]));
+      lin_us += 1000.0 * t;
+      ++lin_n;
     }
     for (auto& e : ev) hipEventDestroy(e);
-    kernel_us[0] = lin_n ? (float)(lin_us / lin_n) : 0.0f;
-    kernel_us[1] = fin_n ? (float)(fin_us / fin_n) : 0.0f;
+    kernel_us[1] = lin_n ? (float)(lin_us / lin_n) : 0.0f;
+    b->result_idx = R & 1;
+    b->last_persistent = false;
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
@@ -743,6 +833,8 @@ extern "C" int picp_one_round(picp_t* h, float threshold, float damping, int min
   HIP_TRY(launch_round(b, 0, 0, 1));
   HIP_TRY(launch_round(b, 1, 1, 0));
   b->last_rounds = 1;
+  b->result_idx = 1;
+  b->last_persistent = false;
   rc = batch_read_results(b);
   if (rc) return rc;
   const PicpState& s = b->result_h[0];

@@ -113,7 +113,7 @@ def lib():
         "picp_batch_solve_async": ([vp, pp], i),
         "picp_batch_sync": ([vp], i),
         "picp_batch_time": ([vp, pp, i, fp, fp], i),
-        "picp_batch_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i)], i),
+        "picp_batch_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "picp_triangulate": ([i, fp, fp, fp, fp, i64, fp], i),
         "picp_projection_matrix": ([fp, fp, fp], i),
     }
@@ -329,8 +329,10 @@ class Batch:
     def info(self):
         tot = ctypes.c_int64(0)
         nb = ctypes.c_int(0)
-        _check(lib().picp_batch_info(self._b, ctypes.byref(tot), ctypes.byref(nb)))
-        return {"total_corr": tot.value, "n_blocks": nb.value}
+        mode = ctypes.c_int(0)
+        _check(lib().picp_batch_info(self._b, ctypes.byref(tot), ctypes.byref(nb), ctypes.byref(mode)))
+        return {"total_corr": tot.value, "n_blocks": nb.value,
+                "mode": "persistent" if mode.value == 1 else "graph"}
 
 
 def projection_matrix(K, T_cw):

@@ -31,9 +31,30 @@ class VOData:
         self.meas_desc = d["meas_desc"]
         self.K = d["K"]
         self.rows = int(d["rows"])
+        self.ref_errors = d["ref_errors"] if "ref_errors" in d else None
         self.cols = int(d["cols"])
         self.n_frames = self.gt_pose.shape[0]
         self._id2row = {int(i): r for r, i in enumerate(self.world_id)}
+
+    def write_reference_format(self, out_dir):
+        """Re-emit data/meas-NNNNN.dat and data/world.dat in the reference's text format
+        (parsed by src/my_utilities.cpp:35-182) for the C++ drop-in driver."""
+        os.makedirs(out_dir, exist_ok=True)
+        for k in range(self.n_frames):
+            f = self.frame(k)
+            with open(os.path.join(out_dir, "meas-%05d.dat" % k), "w") as fh:
+                fh.write("seq: %d\n" % k)
+                fh.write("gt_pose: %r %r %r\n" % tuple(float(x) for x in self.gt_pose[k]))
+                fh.write("odom_pose: %r %r %r\n" % tuple(float(x) for x in self.odom_pose[k]))
+                for i in range(len(f["uv"])):
+                    fh.write("point %d %d %r %r %s\n" % (
+                        int(f["id_meas"][i]), int(f["id_real"][i]), float(f["uv"][i][0]), float(f["uv"][i][1]),
+                        " ".join(repr(float(x)) for x in f["desc"][i])))
+        with open(os.path.join(out_dir, "world.dat"), "w") as fh:
+            for r in range(len(self.world_id)):
+                fh.write("%d %s %s\n" % (int(self.world_id[r]), " ".join(repr(float(x)) for x in self.world_xyz[r]),
+                                         " ".join(repr(float(x)) for x in self.world_desc[r])))
+        return out_dir
 
     def frame(self, k):
         sel = self.meas_frame == k

@@ -100,9 +100,8 @@ def main():
     barrier()
     sync_all()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        b.solve_async(**params)
-    b.sync()
+    # the K timed steps: K graph replays on the library's stream, bracketed by HIP events
+    ev_ms, (launch_us, pair_us) = b.time(args.steps, **params)
     sync_all()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -115,18 +114,19 @@ def main():
     poses = b.poses()
     err = max(synth.se3_log_norm(poses[i], T_gt[i]) for i in range(len(sizes)))
     if dist is not None:
-        mine = torch.tensor(poses.reshape(-1), device="cuda")
-        allp = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allp, mine)  # RCCL over xGMI: the only collective of the batch split
+        from picp_amd.dist import gather_rows
+        # RCCL all-gather over xGMI: the only collective of the batch split (after timing)
+        allp = gather_rows(poses.reshape(len(sizes), 16), world * len(sizes), dist, device="cuda")
+        assert allp.shape == (world * len(sizes), 16)
         errs = torch.tensor([err], dtype=torch.float64, device="cuda")
         dist.all_reduce(errs, op=dist.ReduceOp.MAX)
         err = float(errs.item())
 
-    # ---- per-launch kernel duration (HIP event pairs on the library's stream) ----
-    total_ms, (lin_us, fin_us) = b.time(3, **params)
+    # ---- roofline of the round kernel: algorithmic bytes per launch / mean launch duration,
+    #      the duration from the HIP events around the timed region (launches back to back) ----
     info = b.info()
     corr_per_launch = int(info["total_corr"])
-    achieved = BYTES_PER_CORR * corr_per_launch / (lin_us * 1e-6) / 1e9 if lin_us > 0 else 0.0
+    achieved = BYTES_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
 
     rounds_total = world * len(sizes) * R * args.steps
     value = rounds_total / elapsed
@@ -160,8 +160,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": None,
             "kernel": "picp_round_kernel (linearize launch)",
-            "kernel_us": round(lin_us, 3),
-            "finalize_us": round(fin_us, 3),
+            "kernel_us": round(launch_us, 3),
+            "kernel_us_event_pair": round(pair_us, 3),
+            "timed_region_event_ms": round(ev_ms, 4),
             "bytes_per_launch": BYTES_PER_CORR * corr_per_launch,
             "blocks_per_launch": info["n_blocks"],
         },

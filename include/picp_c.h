@@ -135,14 +135,18 @@ int picp_batch_solve(picp_batch_t* b, const picp_params* params);
 int picp_batch_solve_async(picp_batch_t* b, const picp_params* params);
 int picp_batch_sync(picp_batch_t* b);
 
-/* Time `reps` back-to-back fused solves on the batch's stream with HIP events.
- * total_ms = elapsed of the whole region; kernel_us[0] = mean duration of one linearize
- * round launch (event pairs around each round kernel, separate instrumented pass),
- * kernel_us[1] = mean duration of the finalize launch. */
+/* Run `reps` back-to-back fused solves (graph replays) on the batch's stream between two HIP
+ * events.  total_ms = event time of the whole region; kernel_us[0] = mean launch period of the
+ * round kernel in that region (total / (reps * (max_rounds + 1)) launches); kernel_us[1] =
+ * mean of event pairs around single round launches (separate pass; includes event overhead).
+ * Blocking; results readable with picp_batch_get_poses/stats afterwards. */
 int picp_batch_time(picp_batch_t* b, const picp_params* params, int reps, float* total_ms,
                     float kernel_us[2]);
-/* Number of linearize blocks per launch and total correspondences (introspection). */
-int picp_batch_info(picp_batch_t* b, int64_t* total_corr, int* n_blocks);
+/* Introspection: total correspondences, blocks per launch, and the execution mode chosen for
+ * the batch: 0 = one launch per GN round replayed from a hipGraph (any batch); 1 = the whole
+ * loop in one persistent launch (batches whose blocks all fit on the device at once; env
+ * PICP_MODE=graph forces 0). */
+int picp_batch_info(picp_batch_t* b, int64_t* total_corr, int* n_blocks, int* mode);
 
 /* ---------------- linear triangulation (cv::triangulatePoints replacement) ---------------- */
 

@@ -55,8 +55,11 @@ def main():
     # camera.dat (K and the robot->camera mount); values also hard-coded in src/cam.cpp:11-31
     K = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
     mount = np.array([[0, 0, 1, 0.2], [-1, 0, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1]], np.float32)
+    # the reference's published run (output/errors.txt: frame, translational err, yaw err) -- a
+    # loose end-to-end band only (UB-tainted, OpenCV-RANSAC bootstrap)
+    errs = np.loadtxt(os.path.join(REF, "output", "errors.txt"), dtype=np.float64)
     np.savez_compressed(
-        OUT,
+        OUT, ref_errors=errs.astype(np.float32),
         world_id=np.array(wid, np.int32), world_xyz=np.array(wxyz, np.float32),
         world_desc=np.array(wdesc, np.float32),
         gt_pose=gt, odom_pose=odom,

@@ -199,13 +199,23 @@ def test_batch_ragged_matches_single_and_oracle(native, oracle):
         assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL, i
         assert stats[i]["rounds"] == 50
         if n >= 1000:
-            s = native.PICPSolver()
+            import os
             pr = np.stack([np.arange(n), np.arange(n)], 1).astype(np.int32)
-            s.init(p["T_init"], p["xyz"][:n], p["uv"][:n])
-            s.setKernelThreshold(THR)
-            s.solve(pr, max_rounds=50, conv_eps=-1.0)
-            # same partition and reduction order -> bit-identical to the batched solve
+            os.environ["PICP_MODE"] = "graph"  # the ragged batch runs one launch per round
+            try:
+                s = native.PICPSolver()
+                s.init(p["T_init"], p["xyz"][:n], p["uv"][:n])
+                s.setKernelThreshold(THR)
+                s.solve(pr, max_rounds=50, conv_eps=-1.0)
+            finally:
+                os.environ.pop("PICP_MODE", None)
+            # same mode, partition and reduction order -> bit-identical to the batched solve
             np.testing.assert_array_equal(s.pose(), poses[i])
+            s2 = native.PICPSolver()  # default (persistent) mode: same answer within tolerance
+            s2.init(p["T_init"], p["xyz"][:n], p["uv"][:n])
+            s2.setKernelThreshold(THR)
+            s2.solve(pr, max_rounds=50, conv_eps=-1.0)
+            assert synth.se3_log_norm(s2.pose(), poses[i]) < POSE_TOL
 
 
 def test_solve_is_deterministic(native):
@@ -306,3 +316,69 @@ def test_full_size_c2_c3_properties(native, oracle):
                                          conv_eps=-1.0)
         assert synth.se3_log_norm(T, T_ref) < POSE_TOL
         assert abs(st["n_in"] - st_ref["n_in"]) <= 10
+
+
+def _batch_mode(native, sizes, mode, **kw):
+    import os
+    old = os.environ.get("PICP_MODE")
+    if mode == "graph":
+        os.environ["PICP_MODE"] = "graph"
+    else:
+        os.environ.pop("PICP_MODE", None)
+    try:
+        return native.Batch(sizes, **kw)
+    finally:
+        if old is None:
+            os.environ.pop("PICP_MODE", None)
+        else:
+            os.environ["PICP_MODE"] = old
+
+
+@pytest.mark.parametrize("n,of,keep,conv", [(100000, 0.0, 0, -1.0), (100000, 0.3, 1, -1.0),
+                                            (1000000, 0.3, 0, -1.0), (3000, 0.0, 0, 1e-4),
+                                            (257, 0.0, 0, -1.0), (1, 0.0, 0, -1.0)])
+def test_persistent_and_graph_modes_agree_with_oracle(native, oracle, n, of, keep, conv):
+    """Single-launch persistent solve vs one-launch-per-round graph solve vs the oracle."""
+    synth = _synth()
+    p = synth.make_problem(n, seed=77, outlier_frac=of, pixel_noise=0.5, shuffle=False)
+    res = {}
+    for mode in ("persistent", "graph"):
+        b = _batch_mode(native, [n], mode)
+        assert b.info()["mode"] == mode
+        b.set_data(p["xyz"], p["uv"])
+        b.set_poses(p["T_init"][None])
+        b.solve(threshold=THR, max_rounds=50, conv_eps=conv, keep_outliers=keep)
+        res[mode] = (b.poses()[0], b.stats()[0])
+    T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"], p["y"], p["z"], p["u"], p["v"],
+                                     THR, keep_outliers=keep, mode=oracle.MODE_F64, max_rounds=50,
+                                     conv_eps=conv)
+    for mode, (T, st) in res.items():
+        assert synth.se3_log_norm(T, T_ref) < POSE_TOL, mode
+        assert abs(st["n_in"] - st_ref["n_in"]) <= max(2, n // 100000), mode
+        if conv < 0:
+            assert st["rounds"] == 50
+    assert res["persistent"][1]["rounds"] == res["graph"][1]["rounds"]
+
+
+def test_persistent_uniform_multi_frame_batch(native, oracle):
+    synth = _synth()
+    P, n = 8, 5000
+    bt = synth.make_batch(P, n, base_seed=500, pixel_noise=0.5, outlier_frac=0.1)
+    b = native.Batch(bt["sizes"])
+    assert b.info()["mode"] == "persistent"
+    b.set_data(bt["xyz"], bt["uv"])
+    b.set_poses(bt["T_init"])
+    b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
+    poses, stats = b.poses(), b.stats()
+    for i in range(P):
+        xyz = bt["xyz"][i * n:(i + 1) * n]
+        uv = bt["uv"][i * n:(i + 1) * n]
+        T_ref, st_ref = oracle.solve_soa(bt["T_init"][i], synth.K_REF.astype(np.float32), 480, 640,
+                                         xyz[:, 0].copy(), xyz[:, 1].copy(), xyz[:, 2].copy(),
+                                         uv[:, 0].copy(), uv[:, 1].copy(), THR, mode=oracle.MODE_F64,
+                                         max_rounds=50, conv_eps=1e-5)
+        assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL
+        assert stats[i]["converged"] == int(st_ref["converged"])
+    # repeated replays of the same graph give identical results (granules re-zeroed per launch)
+    b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
+    np.testing.assert_array_equal(b.poses(), poses)

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the persistent kernel (diagnostic stamp build), rounds 11 and 12.
+Stamps: 0 round start, 1 partial published, 2 leader: sweep done / others: pose received,
+3 leader: solve done."""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "02-visualodometry_amd"))
+os.environ["PICP_LIB"] = os.path.join(ROOT, "02-visualodometry_amd", "lib", "libpicp_amd_stamps.so")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100000)
+    args = ap.parse_args()
+    import numpy as np
+    import picp_amd
+    from picp_amd import synth
+    p = synth.make_problem(args.n, seed=42, pixel_noise=0.5, shuffle=False)
+    b = picp_amd.Batch([args.n])
+    info = b.info()
+    assert info["mode"] == "persistent", info
+    b.set_data(p["xyz"], p["uv"])
+    b.set_poses(p["T_init"][None])
+    for _ in range(3):
+        b.solve(threshold=3000.0, max_rounds=50, conv_eps=-1.0)
+    nb = info["n_blocks"]
+    L = picp_amd.lib()
+    L.picp_debug_pstamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    buf = np.zeros((2, 256, 8), np.uint64)
+    assert L.picp_debug_pstamps(buf.ctypes.data, buf.size) == 0
+    for r in (0, 1):
+        st = buf[r, :nb].astype(np.int64)
+        t0 = st[:, 0].min()
+        rel = (st - t0) * 10
+        print("round %d (%d blocks), ns from first round start" % (11 + r, nb))
+        print("  leader: start %d published %d swept(all threads) %d combined %d solve_start %d solve_end %d" % (rel[0,0], rel[0,1], rel[0,2], rel[0,3], rel[0,4], rel[0,5]))
+        others = rel[1:]
+        for k, nm in enumerate(["start", "published", "pose_received"]):
+            print("  others %-14s median %6d  min %6d  max %6d" % (nm, np.median(others[:, k]), others[:, k].min(), others[:, k].max()))
+    nxt = (buf[1, :nb, 0].astype(np.int64).min() - buf[0, :nb, 0].astype(np.int64).min()) * 10
+    print("round period (first start r11 -> first start r12): %d ns" % nxt)
+
+
+if __name__ == "__main__":
+    main()

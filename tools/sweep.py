@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--interleave", type=int, default=3)
     ap.add_argument("--outlier", type=float, default=0.0)
+    ap.add_argument("--env", default="PICP_ITEMS_PER_BLOCK", help="env var the --ipb values are written to")
     args = ap.parse_args()
     import numpy as np
     import picp_amd
@@ -34,13 +35,13 @@ def main():
         xyz, uv, Ti, sizes = bt["xyz"], bt["uv"], bt["T_init"], bt["sizes"]
     batches = {}
     for ipb in [int(x) for x in args.ipb.split(",")]:
-        os.environ["PICP_ITEMS_PER_BLOCK"] = str(ipb)
+        os.environ[args.env] = str(ipb)
         b = picp_amd.Batch(sizes)
         b.set_data(xyz, uv)
         b.set_poses(Ti)
         b.solve(threshold=3000.0, max_rounds=args.rounds, conv_eps=-1.0)  # warm (graph build)
         batches[ipb] = b
-    os.environ.pop("PICP_ITEMS_PER_BLOCK", None)
+    os.environ.pop(args.env, None)
     res = {k: [] for k in batches}
     kus = {}
     for _ in range(args.interleave):
@@ -52,10 +53,10 @@ def main():
     for ipb, v in res.items():
         ms = float(np.median(v))
         it_s = len(sizes) * args.rounds / (ms * 1e-3)
-        print(json.dumps({"ipb": ipb, "blocks": batches[ipb].info()["n_blocks"], "ms_per_solve": round(ms, 4),
+        print(json.dumps({args.env: ipb, "blocks": batches[ipb].info()["n_blocks"], "mode": batches[ipb].info()["mode"], "ms_per_solve": round(ms, 4),
                           "us_per_round": round(1000 * ms / (args.rounds + 1), 3),
-                          "iter_per_s": round(it_s, 1), "lin_us": round(kus[ipb][0], 3),
-                          "fin_us": round(kus[ipb][1], 3),
+                          "iter_per_s": round(it_s, 1), "launch_us": round(kus[ipb][0], 3),
+                          "pair_us": round(kus[ipb][1], 3),
                           "GBps_alg": round(20 * corr / (kus[ipb][0] * 1e-6) / 1e9, 1),
                           "pose_err": synth.se3_log_norm(batches[ipb].poses()[0], Ti[0] * 0 + (p["T_gt"] if args.problems == 1 else bt["T_gt"][0]))}))
 
