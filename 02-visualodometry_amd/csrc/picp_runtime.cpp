@@ -33,6 +33,12 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              const PicpState* st_in, PicpState* st_out,
                                              unsigned long long* gpart, unsigned long long* gpose,
                                              unsigned int* err, unsigned long long timeout_ticks);
+extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
+                                        const float* Y, const float* Z, const float* U,
+                                        const float* V, const PicpArgs* args,
+                                        const PicpProblem* probs, const PicpState* st_in,
+                                        PicpState* st_out);
+extern "C" int picp_block_max_items(void);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -123,6 +129,7 @@ static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 #define PICP_MODE_GRAPH 0
 #define PICP_MODE_PERSISTENT 1
+#define PICP_MODE_BLOCK 2
 #define PICP_POSE_GRAN 16
 #define PICP_MAX_PBLK 256
 
@@ -218,25 +225,63 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     if (offs[i + 1] - offs[i] != offs[1] - offs[0]) b->uniform = 0;
   b->n_u = (int)(offs[1] - offs[0]);
   b->stride_u = round_up(b->n_u, 4);
-  // Persistent single launch when every block of the batch can be resident at once (one block
-  // per CU, each lane holding <= 16 correspondences in registers); otherwise a launch per round.
+  // Execution mode:
+  //  * BLOCK      -- one block per problem, all rounds in-block, problem held in registers:
+  //                  batches of >= 2 problems of <= picp_block_max_items() correspondences;
+  //  * PERSISTENT -- one launch, blocks of one problem hand off through granules: when every
+  //                  block of the batch is resident at once (uniform problems);
+  //  * GRAPH      -- one launch per round, replayed from a hipGraph: everything else.
+  // PICP_MODE=graph|persistent|block forces a mode when the batch is eligible for it.
   int ipb = items_per_block(b->total);
   b->mode = PICP_MODE_GRAPH;
   {
     const char* m = getenv("PICP_MODE");
-    const bool allow = !(m && strcmp(m, "graph") == 0);
-    int bpp = b->num_cu / np;  // blocks per problem available
-    if (const char* e = getenv("PICP_PERSIST_BLOCKS")) bpp = std::max(1, std::min(bpp, atoi(e)));
-    if (allow && b->uniform && bpp >= 1) {
-      const int64_t per_block = std::max<int64_t>(1, (b->n_u + bpp - 1) / bpp);
-      int npt = 1;
-      while ((int64_t)npt * PICP_BLOCK < per_block && npt < 32) npt *= 2;
-      const int nb = (int)std::max<int64_t>(1, (b->n_u + (int64_t)npt * PICP_BLOCK - 1) / ((int64_t)npt * PICP_BLOCK));
-      if (npt <= 16 && nb <= PICP_MAX_PBLK && (int64_t)nb * np <= b->num_cu) {
-        b->mode = PICP_MODE_PERSISTENT;
-        b->npt = npt;
-        ipb = npt * PICP_BLOCK;
+    const bool force_graph = m && strcmp(m, "graph") == 0;
+    const bool force_persist = m && strcmp(m, "persistent") == 0;
+    const bool force_block = m && strcmp(m, "block") == 0;
+    int64_t max_n = 0;
+    for (int i = 0; i < np; ++i) max_n = std::max<int64_t>(max_n, offs[i + 1] - offs[i]);
+    int bnpt = 0;  // block mode: register-resident correspondences per lane (rest streamed)
+    {
+      int cap = picp_block_max_items() / 512;
+      if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
+      bnpt = 1;
+      while (bnpt < cap && (int64_t)bnpt * 512 < max_n) bnpt *= 2;
+      // one block per problem: only sensible while a problem is small enough for one CU
+      if (max_n > ((int64_t)1 << 16)) bnpt = 0;
+    }
+    int pnpt = 0, pnb = 0;  // persistent mode partition
+    {
+      int bpp = b->num_cu / np;  // blocks per problem available
+      if (const char* e = getenv("PICP_PERSIST_BLOCKS")) bpp = std::max(1, std::min(bpp, atoi(e)));
+      if (b->uniform && bpp >= 1) {
+        const int64_t per_block = std::max<int64_t>(1, (b->n_u + bpp - 1) / bpp);
+        int npt = 1;
+        while ((int64_t)npt * PICP_BLOCK < per_block && npt < 32) npt *= 2;
+        const int nb = (int)std::max<int64_t>(1, (b->n_u + (int64_t)npt * PICP_BLOCK - 1) / ((int64_t)npt * PICP_BLOCK));
+        if (npt <= 16 && nb <= PICP_MAX_PBLK && (int64_t)nb * np <= b->num_cu) {
+          pnpt = npt;
+          pnb = nb;
+        }
       }
+    }
+    (void)pnb;
+    if (force_graph) {
+      b->mode = PICP_MODE_GRAPH;
+    } else if (force_block && bnpt) {
+      b->mode = PICP_MODE_BLOCK;
+    } else if (force_persist && pnpt) {
+      b->mode = PICP_MODE_PERSISTENT;
+    } else if (np >= 2 && bnpt) {
+      b->mode = PICP_MODE_BLOCK;
+    } else if (pnpt) {
+      b->mode = PICP_MODE_PERSISTENT;
+    }
+    if (b->mode == PICP_MODE_PERSISTENT) {
+      b->npt = pnpt;
+      ipb = pnpt * PICP_BLOCK;
+    } else if (b->mode == PICP_MODE_BLOCK) {
+      b->npt = bnpt;
     }
   }
   b->ipb = ipb;
@@ -367,6 +412,9 @@ static hipError_t launch_round(picp_batch* b, int j, int fin, int in_buf) {
 
 // Enqueue the R+1 launches (plus the initial-state copy) of a fused solve on the stream.
 static hipError_t enqueue_solve(picp_batch* b, int R) {
+  if (b->mode == PICP_MODE_BLOCK)
+    return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
+                             b->probs_d, b->init_d, b->st_d[0]);
   if (b->mode == PICP_MODE_PERSISTENT) {
     // every polled word (error word and all granules) is zeroed before each launch
     hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
@@ -411,7 +459,7 @@ static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   if (rc) return rc;
   HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
   b->last_rounds = R;
-  b->result_idx = (b->mode == PICP_MODE_PERSISTENT) ? 0 : (R & 1);
+  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? (R & 1) : 0;
   b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
   return PICP_OK;
 }
@@ -593,7 +641,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
   HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
   if (total_ms) *total_ms = ms;
   b->last_rounds = R;
-  b->result_idx = (b->mode == PICP_MODE_PERSISTENT) ? 0 : (R & 1);
+  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? (R & 1) : 0;
   b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
   if (kernel_us) {
     // [0]: mean launch period of the round kernel inside the replayed graphs (event time over
@@ -601,9 +649,9 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
     //      the per-launch duration a kernel trace reports);
     // [1]: mean of event pairs around single launches of the same solve (an upper bound: it
     //      adds the event overhead to every launch).
-    const int launches = (b->mode == PICP_MODE_PERSISTENT) ? 1 : (R + 1);
+    const int launches = (b->mode == PICP_MODE_GRAPH) ? (R + 1) : 1;
     kernel_us[0] = 1000.0f * ms / (float)(reps * launches);
-    if (b->mode == PICP_MODE_PERSISTENT) {
+    if (b->mode != PICP_MODE_GRAPH) {
       hipEvent_t a0, a1;
       HIP_TRY(hipEventCreate(&a0));
       HIP_TRY(hipEventCreate(&a1));
@@ -619,6 +667,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
       hipEventDestroy(e0);
       hipEventDestroy(e1);
       b->result_idx = 0;
+      b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
       return batch_read_results(b);
     }
     std::vector<hipEvent_t> ev((size_t)(R + 2));

@@ -332,7 +332,7 @@ class Batch:
         mode = ctypes.c_int(0)
         _check(lib().picp_batch_info(self._b, ctypes.byref(tot), ctypes.byref(nb), ctypes.byref(mode)))
         return {"total_corr": tot.value, "n_blocks": nb.value,
-                "mode": "persistent" if mode.value == 1 else "graph"}
+                "mode": {0: "graph", 1: "persistent", 2: "block"}[mode.value]}
 
 
 def projection_matrix(K, T_cw):

@@ -180,14 +180,16 @@ def test_points_behind_camera_and_outside_image_are_skipped(native, oracle):
     _lin_close(got, ref)
 
 
-def test_batch_ragged_matches_single_and_oracle(native, oracle):
+@pytest.mark.parametrize("mode", ["graph", "block"])
+def test_batch_ragged_matches_single_and_oracle(native, oracle, mode):
     synth = _synth()
     sizes = [0, 1, 3, 1000, 5000, 20001, 1024, 4097]
     probs = [synth.make_problem(max(n, 1), seed=100 + i, outlier_frac=0.1, pixel_noise=0.5, shuffle=False)
              for i, n in enumerate(sizes)]
     xyz = np.concatenate([p["xyz"][:n] for p, n in zip(probs, sizes)])
     uv = np.concatenate([p["uv"][:n] for p, n in zip(probs, sizes)])
-    b = native.Batch(sizes)
+    b = _batch_mode(native, sizes, mode)
+    assert b.info()["mode"] == mode
     b.set_data(xyz, uv)
     b.set_poses(np.stack([p["T_init"] for p in probs]))
     b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
@@ -198,10 +200,11 @@ def test_batch_ragged_matches_single_and_oracle(native, oracle):
                                          mode=oracle.MODE_F64, max_rounds=50, conv_eps=-1.0)
         assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL, i
         assert stats[i]["rounds"] == 50
-        if n >= 1000:
+        assert abs(stats[i]["n_in"] - st_ref["n_in"]) <= 2
+        if n >= 1000 and mode == "graph":
             import os
             pr = np.stack([np.arange(n), np.arange(n)], 1).astype(np.int32)
-            os.environ["PICP_MODE"] = "graph"  # the ragged batch runs one launch per round
+            os.environ["PICP_MODE"] = "graph"  # same mode as the batch
             try:
                 s = native.PICPSolver()
                 s.init(p["T_init"], p["xyz"][:n], p["uv"][:n])
@@ -321,10 +324,7 @@ def test_full_size_c2_c3_properties(native, oracle):
 def _batch_mode(native, sizes, mode, **kw):
     import os
     old = os.environ.get("PICP_MODE")
-    if mode == "graph":
-        os.environ["PICP_MODE"] = "graph"
-    else:
-        os.environ.pop("PICP_MODE", None)
+    os.environ["PICP_MODE"] = mode
     try:
         return native.Batch(sizes, **kw)
     finally:
@@ -360,12 +360,13 @@ def test_persistent_and_graph_modes_agree_with_oracle(native, oracle, n, of, kee
     assert res["persistent"][1]["rounds"] == res["graph"][1]["rounds"]
 
 
-def test_persistent_uniform_multi_frame_batch(native, oracle):
+@pytest.mark.parametrize("mode,P,n", [("persistent", 8, 5000), ("block", 8, 5000), ("block", 6, 20000),
+                                      ("graph", 8, 5000)])
+def test_uniform_multi_frame_batch_modes(native, oracle, mode, P, n):
     synth = _synth()
-    P, n = 8, 5000
     bt = synth.make_batch(P, n, base_seed=500, pixel_noise=0.5, outlier_frac=0.1)
-    b = native.Batch(bt["sizes"])
-    assert b.info()["mode"] == "persistent"
+    b = _batch_mode(native, bt["sizes"], mode)
+    assert b.info()["mode"] == mode
     b.set_data(bt["xyz"], bt["uv"])
     b.set_poses(bt["T_init"])
     b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)

@@ -34,7 +34,7 @@ def main():
         bt = synth.make_batch(args.problems, args.n, outlier_frac=args.outlier, pixel_noise=0.5)
         xyz, uv, Ti, sizes = bt["xyz"], bt["uv"], bt["T_init"], bt["sizes"]
     batches = {}
-    for ipb in [int(x) for x in args.ipb.split(",")]:
+    for ipb in args.ipb.split(","):
         os.environ[args.env] = str(ipb)
         b = picp_amd.Batch(sizes)
         b.set_data(xyz, uv)
