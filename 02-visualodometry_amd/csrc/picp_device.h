@@ -238,28 +238,19 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
   small_sincos(dx[3], &sa, &ca);
   small_sincos(dx[4], &sb, &cb);
   small_sincos(dx[5], &sc, &cc);
-  const float Rx[3][3] = {{1.f, 0.f, 0.f}, {0.f, ca, -sa}, {0.f, sa, ca}};
-  const float Ry[3][3] = {{cb, 0.f, sb}, {0.f, 1.f, 0.f}, {-sb, 0.f, cb}};
-  const float Rz[3][3] = {{cc, -sc, 0.f}, {sc, cc, 0.f}, {0.f, 0.f, 1.f}};
-  float Rxy[3][3], Rd[3][3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = Rx[i][0] * Ry[0][j];
-      s = s + Rx[i][1] * Ry[1][j];
-      s = s + Rx[i][2] * Ry[2][j];
-      Rxy[i][j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = Rxy[i][0] * Rz[0][j];
-      s = s + Rxy[i][1] * Rz[1][j];
-      s = s + Rxy[i][2] * Rz[2][j];
-      Rd[i][j] = s;
-    }
+  // Rd = Rx(a)*Ry(b)*Rz(c) in closed form: the same products and sums as the 3x3 products
+  // of src/defs.h:133 with their structural zeros and ones folded away (x*1 = x, x+0 = x).
+  const float sasb = sa * sb, casb = ca * sb;
+  float Rd[3][3];
+  Rd[0][0] = cb * cc;
+  Rd[0][1] = -(cb * sc);
+  Rd[0][2] = sb;
+  Rd[1][0] = sasb * cc + ca * sc;
+  Rd[1][1] = ca * cc - sasb * sc;
+  Rd[1][2] = -(sa * cb);
+  Rd[2][0] = sa * sc - casb * cc;
+  Rd[2][1] = casb * sc + sa * cc;
+  Rd[2][2] = ca * cb;
   float Rn[9], tn[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {

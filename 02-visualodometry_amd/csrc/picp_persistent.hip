@@ -25,6 +25,7 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 #define PICP_MAX_PBLK 256   // max blocks per problem in this mode (sweep registers)
+#define PICP_PBLOCK 512     // threads per block: 8 waves, 2 per SIMD (<= 256 VGPRs)
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
 
 // Diagnostic build only (-DPICP_STAMPS): s_memrealtime per phase of rounds (epochs) 11 and 12.
@@ -51,15 +52,15 @@ __device__ __forceinline__ bool timed_out(unsigned long long deadline) {
 }
 
 template <int NPT>
-__global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
+__global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
     unsigned long long* gpart, unsigned long long* gpose, unsigned int* err,
     unsigned long long timeout_ticks) {
-  __shared__ double s_red[8][PICP_NPART + 1];
+  __shared__ double s_red[PICP_PBLOCK / 32][PICP_NPART + 1];
   __shared__ double s_tot[PICP_NPART];
-  __shared__ float s_wave[PICP_BLOCK / 64][PICP_NPART];
+  __shared__ float s_wave[PICP_PBLOCK / 64][PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
   __shared__ PicpState s_st;
@@ -72,8 +73,11 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
   const int count = max(0, min(A.ipb, A.n_u - first));
   const int64_t base = (int64_t)p * A.stride_u + first;
   const bool leader = (kb == 0);
-  gu64_t* my_part = ((gu64_t*)gpart) + (size_t)blockIdx.x * PICP_NPART;
-  gu64_t* prob_part = ((gu64_t*)gpart) + (size_t)p * nblk * PICP_NPART;
+  // partial granules are double-buffered by round parity, so correctness does not rest on the
+  // leader having swept round r before any block publishes round r+1
+  const size_t part_stride = (size_t)gridDim.x * PICP_NPART;
+  gu64_t* my_part0 = ((gu64_t*)gpart) + (size_t)blockIdx.x * PICP_NPART;
+  gu64_t* prob_part0 = ((gu64_t*)gpart) + (size_t)p * nblk * PICP_NPART;
   gu64_t* prob_pose = ((gu64_t*)gpose) + (size_t)p * PICP_POSE_GRAN;
   gu32_t* errw = ((gu32_t*)err);
 
@@ -81,7 +85,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int i = tid + k * PICP_BLOCK;
+    const int i = tid + k * PICP_PBLOCK;
     const int ic = min(i, max(count - 1, 0));
     xs[k] = X[base + ic];
     ys[k] = Y[base + ic];
@@ -104,10 +108,8 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
 #pragma unroll
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
     s_done = s.done;
-    if (leader) {
-      s_st = s;
-      if (s.done) st_out[p] = s;
-    }
+    s_st = s;
+    if (leader && s.done) st_out[p] = s;
   }
   __syncthreads();
   const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
     a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
 #pragma unroll
     for (int k = 0; k < NPT; ++k)
-      accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], tid + k * PICP_BLOCK < count, a);
+      accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], tid + k * PICP_PBLOCK < count, a);
     float v[PICP_NPART];
 #pragma unroll
     for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
@@ -154,23 +156,24 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
     if (tid < PICP_NPART) {
       float sum = s_wave[0][tid];
 #pragma unroll
-      for (int w = 1; w < PICP_BLOCK / 64; ++w) sum += s_wave[w][tid];
-      __hip_atomic_store(my_part + tid, granule(epoch, sum), RLX_AGENT);
+      for (int w = 1; w < PICP_PBLOCK / 64; ++w) sum += s_wave[w][tid];
+      __hip_atomic_store(my_part0 + (epoch & 1) * part_stride + tid, granule(epoch, sum), RLX_AGENT);
     }
     PSTAMP(1);
 
     if (leader) {
       // ---- 2. sweep the problem's partials (entry e = tid&31 of blocks (tid>>5) + 8i) ----
       const int e = tid & 31, g = tid >> 5;
-      constexpr int MAXG = PICP_MAX_PBLK / (PICP_BLOCK / 32);
+      constexpr int NG = PICP_PBLOCK / 32;  // block groups swept in parallel
+      constexpr int MAXG = PICP_MAX_PBLK / NG;
       unsigned long long gv[MAXG];
       bool ok = false;
       for (;;) {
         ok = true;
 #pragma unroll
         for (int i = 0; i < MAXG; ++i) {
-          const int b = g + 8 * i;
-          gv[i] = __hip_atomic_load(prob_part + (size_t)min(b, nblk - 1) * PICP_NPART + e, RLX_AGENT);
+          const int b = g + NG * i;
+          gv[i] = __hip_atomic_load(prob_part0 + (epoch & 1) * part_stride + (size_t)min(b, nblk - 1) * PICP_NPART + e, RLX_AGENT);
           ok &= (b >= nblk) || ((unsigned)(gv[i] >> 32) == epoch);
         }
         if (ok) break;
@@ -183,14 +186,14 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
       double acc = 0.0;
 #pragma unroll
       for (int i = 0; i < MAXG; ++i)
-        if (g + 8 * i < nblk) acc += (double)__uint_as_float((unsigned)gv[i]);
+        if (g + NG * i < nblk) acc += (double)__uint_as_float((unsigned)gv[i]);
       s_red[g][e] = acc;
       __syncthreads();
       PSTAMP(2);
       if (tid < PICP_NPART) {
         double t = 0.0;
 #pragma unroll
-        for (int gg = 0; gg < PICP_BLOCK / 32; ++gg) t += s_red[gg][tid];
+        for (int gg = 0; gg < NG; ++gg) t += s_red[gg][tid];
         s_tot[tid] = t;
       }
       __syncthreads();
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_persistent_kernel(
 #pragma unroll
         for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
         s_done = ns.done;
-        if (ns.done) st_out[p] = ns;
+        if (ns.done && leader) st_out[p] = ns;
       }
       __syncthreads();
       PSTAMP(3);
@@ -255,6 +258,8 @@ extern "C" hipError_t picp_debug_pstamps(unsigned long long* out, size_t n_words
 #endif
 
 // ------------------------------- host launch wrapper -------------------------------
+extern "C" int picp_persistent_block(void) { return PICP_PBLOCK; }
+
 extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int npt, const float* X,
                                              const float* Y, const float* Z, const float* U,
                                              const float* V, const PicpArgs* args,
@@ -262,15 +267,14 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              unsigned long long* gpart, unsigned long long* gpose,
                                              unsigned int* err, unsigned long long timeout_ticks) {
   if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
-#define PICP_LAUNCH_P(N)                                                                              \
-  hipLaunchKernelGGL(picp_persistent_kernel<N>, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U, \
+#define PICP_LAUNCH_P(N)                                                                             \
+  hipLaunchKernelGGL(picp_persistent_kernel<N>, dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, U, \
                      V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks)
   switch (npt) {
     case 1: PICP_LAUNCH_P(1); break;
     case 2: PICP_LAUNCH_P(2); break;
     case 4: PICP_LAUNCH_P(4); break;
     case 8: PICP_LAUNCH_P(8); break;
-    case 16: PICP_LAUNCH_P(16); break;
     default: return hipErrorInvalidValue;
   }
 #undef PICP_LAUNCH_P

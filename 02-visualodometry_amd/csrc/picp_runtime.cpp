@@ -39,6 +39,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
                                         const PicpProblem* probs, const PicpState* st_in,
                                         PicpState* st_out);
 extern "C" int picp_block_max_items(void);
+extern "C" int picp_persistent_block(void);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -254,12 +255,13 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     {
       int bpp = b->num_cu / np;  // blocks per problem available
       if (const char* e = getenv("PICP_PERSIST_BLOCKS")) bpp = std::max(1, std::min(bpp, atoi(e)));
+      const int pbs = picp_persistent_block();
       if (b->uniform && bpp >= 1) {
         const int64_t per_block = std::max<int64_t>(1, (b->n_u + bpp - 1) / bpp);
         int npt = 1;
-        while ((int64_t)npt * PICP_BLOCK < per_block && npt < 32) npt *= 2;
-        const int nb = (int)std::max<int64_t>(1, (b->n_u + (int64_t)npt * PICP_BLOCK - 1) / ((int64_t)npt * PICP_BLOCK));
-        if (npt <= 16 && nb <= PICP_MAX_PBLK && (int64_t)nb * np <= b->num_cu) {
+        while ((int64_t)npt * pbs < per_block && npt < 32) npt *= 2;
+        const int nb = (int)std::max<int64_t>(1, (b->n_u + (int64_t)npt * pbs - 1) / ((int64_t)npt * pbs));
+        if (npt <= 8 && nb <= PICP_MAX_PBLK && (int64_t)nb * np <= b->num_cu) {
           pnpt = npt;
           pnb = nb;
         }
@@ -279,7 +281,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     }
     if (b->mode == PICP_MODE_PERSISTENT) {
       b->npt = pnpt;
-      ipb = pnpt * PICP_BLOCK;
+      ipb = pnpt * picp_persistent_block();
     } else if (b->mode == PICP_MODE_BLOCK) {
       b->npt = bnpt;
     }
@@ -333,7 +335,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     b->np_cap = np;
   }
   if (b->mode == PICP_MODE_PERSISTENT) {
-    b->sync_bytes = (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + (int64_t)nblk * PICP_NPART * 8, 256);
+    b->sync_bytes = (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
       b->sync = nullptr;
