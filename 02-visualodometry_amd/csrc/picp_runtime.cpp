@@ -40,6 +40,14 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
                                         PicpState* st_out);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_persistent_block(void);
+struct MatchProblem {
+  int64_t q_off, nq, r_off, nr;
+};
+extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
+                                        const float* q_desc, const float* r_desc,
+                                        const MatchProblem* probs, int dim, float dist_thr,
+                                        float ratio_thr, int32_t* best_idx, float* best_dist,
+                                        float* second_dist, int32_t* accepted);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -1010,4 +1018,67 @@ extern "C" int picp_triangulate(int device, const float P1[12], const float P2[1
   hipFree(buf);
   if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_triangulate: %s", hipGetErrorString(e));
   return PICP_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// descriptor matching (match_points, src/my_utilities.h:70-120)
+// ------------------------------------------------------------------------------------
+extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1, const int64_t* off2,
+                                const float* desc1, const float* desc2, int dim, float dist_thr,
+                                float ratio_thr, int32_t* best_idx, float* best_dist,
+                                float* second_dist, int32_t* accepted) {
+  CHECK_ARG(n_problems >= 1 && n_problems <= 65535 && off1 && off2, "picp_match_batch: bad problem table");
+  CHECK_ARG(dim >= 1 && dim <= 32, "picp_match_batch: dim must be in [1, 32]");
+  for (int i = 0; i < n_problems; ++i)
+    CHECK_ARG(off1[0] == 0 && off2[0] == 0 && off1[i + 1] >= off1[i] && off2[i + 1] >= off2[i],
+              "picp_match_batch: offsets must be prefix sums from 0");
+  const int64_t n1 = off1[n_problems], n2 = off2[n_problems];
+  CHECK_ARG((n1 == 0 || (desc1 && best_idx && best_dist && second_dist && accepted)) && (n2 == 0 || desc2),
+            "picp_match_batch: null array");
+  if (n1 == 0) return PICP_OK;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  CHECK_ARG(device >= 0 && device < ndev, "picp_match_batch: no such HIP device");
+  HIP_TRY(hipSetDevice(device));
+  std::vector<MatchProblem> probs((size_t)n_problems);
+  int64_t max_nq = 0;
+  for (int i = 0; i < n_problems; ++i) {
+    probs[i] = MatchProblem{off1[i], off1[i + 1] - off1[i], off2[i], off2[i + 1] - off2[i]};
+    max_nq = std::max(max_nq, probs[i].nq);
+  }
+  const size_t b_probs = probs.size() * sizeof(MatchProblem);
+  const size_t b_d1 = (size_t)n1 * dim * sizeof(float), b_d2 = (size_t)std::max<int64_t>(n2, 1) * dim * sizeof(float);
+  const size_t b_out = (size_t)n1 * 4;
+  char* buf = nullptr;
+  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + 64));
+  char* cur = buf;
+  auto carve = [&](size_t bytes) { char* r = cur; cur += (bytes + 15) / 16 * 16; return r; };
+  MatchProblem* d_probs = (MatchProblem*)carve(b_probs);
+  float* d_d1 = (float*)carve(b_d1);
+  float* d_d2 = (float*)carve(b_d2);
+  int32_t* d_bi = (int32_t*)carve(b_out);
+  float* d_bd = (float*)carve(b_out);
+  float* d_sd = (float*)carve(b_out);
+  int32_t* d_acc = (int32_t*)carve(b_out);
+  hipError_t e = hipMemcpy(d_probs, probs.data(), b_probs, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_d1, desc1, b_d1, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n2) e = hipMemcpy(d_d2, desc2, (size_t)n2 * dim * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = picp_launch_match(nullptr, n_problems, max_nq, d_d1, d_d2, d_probs, dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc);
+  if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(accepted, d_acc, b_out, hipMemcpyDeviceToHost);
+  hipFree(buf);
+  if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_match_batch: %s", hipGetErrorString(e));
+  return PICP_OK;
+}
+
+extern "C" int picp_match(int device, const float* desc1, int64_t n1, const float* desc2, int64_t n2,
+                          int dim, float dist_thr, float ratio_thr, int32_t* best_idx,
+                          float* best_dist, float* second_dist, int32_t* accepted) {
+  CHECK_ARG(n1 >= 0 && n2 >= 0, "picp_match: negative size");
+  const int64_t o1[2] = {0, n1}, o2[2] = {0, n2};
+  return picp_match_batch(device, 1, o1, o2, desc1, desc2, dim, dist_thr, ratio_thr, best_idx, best_dist,
+                          second_dist, accepted);
 }

@@ -40,7 +40,7 @@ EXPORTED = [
     "picp_batch_set_data", "picp_batch_set_data_device", "picp_batch_set_poses",
     "picp_batch_get_poses", "picp_batch_get_stats", "picp_batch_solve",
     "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_info",
-    "picp_triangulate", "picp_projection_matrix",
+    "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
 ]
 
 
@@ -116,6 +116,10 @@ def lib():
         "picp_batch_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "picp_triangulate": ([i, fp, fp, fp, fp, i64, fp], i),
         "picp_projection_matrix": ([fp, fp, fp], i),
+        "picp_match": ([i, fp, i64, fp, i64, i, f, f, ctypes.POINTER(ctypes.c_int32), fp, fp,
+                        ctypes.POINTER(ctypes.c_int32)], i),
+        "picp_match_batch": ([i, i, ctypes.POINTER(i64), ctypes.POINTER(i64), fp, fp, i, f, f,
+                              ctypes.POINTER(ctypes.c_int32), fp, fp, ctypes.POINTER(ctypes.c_int32)], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -348,3 +352,47 @@ def triangulate(P1, P2, uv1, uv2, device=0):
     _check(lib().picp_triangulate(device, _fptr(_f32(P1, (12,))), _fptr(_f32(P2, (12,))),
                                   _fptr(uv1), _fptr(uv2), uv1.shape[0], _fptr(out)))
     return out
+
+
+def _i32ptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def match_points(desc1, desc2, dist_thr=0.2, ratio_thr=0.8, device=0):
+    """match_points (src/my_utilities.h:70-120) on the GPU -> dict(best_idx, best_dist,
+    second_dist, accepted); the reference's correspondences are the accepted (i, best_idx[i])."""
+    d1 = np.ascontiguousarray(desc1, np.float32)
+    d2 = np.ascontiguousarray(desc2, np.float32)
+    n1 = d1.shape[0]
+    dim = d1.shape[1] if d1.ndim == 2 and d1.shape[1] else (d2.shape[1] if d2.ndim == 2 else 10)
+    n2 = d2.shape[0] if d2.size else 0
+    bi = np.zeros(n1, np.int32)
+    bd = np.zeros(n1, np.float32)
+    sd = np.zeros(n1, np.float32)
+    acc = np.zeros(n1, np.int32)
+    _check(lib().picp_match(device, _fptr(d1), n1, _fptr(d2) if n2 else None, n2, dim, dist_thr, ratio_thr,
+                            _i32ptr(bi), _fptr(bd), _fptr(sd), _i32ptr(acc)))
+    return {"best_idx": bi, "best_dist": bd, "second_dist": sd, "accepted": acc.astype(bool)}
+
+
+def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, device=0):
+    """Many (set 1, set 2) pairs in one launch; returns a list of per-problem dicts."""
+    o1 = np.zeros(len(desc1_list) + 1, np.int64)
+    o2 = np.zeros(len(desc2_list) + 1, np.int64)
+    o1[1:] = np.cumsum([len(d) for d in desc1_list])
+    o2[1:] = np.cumsum([len(d) for d in desc2_list])
+    dim = next((np.asarray(d).shape[1] for d in list(desc1_list) + list(desc2_list) if len(d)), 10)
+    d1 = np.ascontiguousarray(np.concatenate([np.asarray(d, np.float32).reshape(-1, dim) for d in desc1_list]))
+    d2 = np.ascontiguousarray(np.concatenate([np.asarray(d, np.float32).reshape(-1, dim) for d in desc2_list]))
+    n1 = int(o1[-1])
+    bi = np.zeros(n1, np.int32)
+    bd = np.zeros(n1, np.float32)
+    sd = np.zeros(n1, np.float32)
+    acc = np.zeros(n1, np.int32)
+    _check(lib().picp_match_batch(device, len(desc1_list), o1.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                  o2.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _fptr(d1),
+                                  _fptr(d2) if d2.size else None, dim, dist_thr, ratio_thr,
+                                  _i32ptr(bi), _fptr(bd), _fptr(sd), _i32ptr(acc)))
+    return [{"best_idx": bi[o1[i]:o1[i + 1]], "best_dist": bd[o1[i]:o1[i + 1]],
+             "second_dist": sd[o1[i]:o1[i + 1]], "accepted": acc[o1[i]:o1[i + 1]].astype(bool)}
+            for i in range(len(desc1_list))]

@@ -12,9 +12,11 @@ Multi-GPU (torchrun, one process per GPU): every rank solves its own independent
 after timing (RCCL all_gather) to check them.
 
 Printed JSON also carries:
-  roofline     : dominant kernel = picp_round_kernel (linearize launch); achieved = 20 algorithmic
-                 bytes per correspondence (x,y,z,u,v float32 SoA) x N / mean launch duration,
-                 the launch duration measured with HIP event pairs on the library's stream.
+  roofline     : the dominant kernel of the chosen execution mode (persistent: the whole 50-round
+                 solve in one launch; graph: one launch per round); achieved = 20 algorithmic bytes
+                 per correspondence-round (x,y,z,u,v float32 SoA) x correspondence-rounds per launch
+                 / mean launch duration, the duration from HIP events around the timed replays on
+                 the library's stream.
   cpu_baseline : the oracle's faithful float32 single-thread restatement (kind "port"), timed on
                  this host on a bounded sample of the same workload.
 """
@@ -125,7 +127,9 @@ def main():
     # ---- roofline of the round kernel: algorithmic bytes per launch / mean launch duration,
     #      the duration from the HIP events around the timed region (launches back to back) ----
     info = b.info()
-    corr_per_launch = int(info["total_corr"])
+    # graph mode: one launch = one round over every correspondence; persistent/block mode: one
+    # launch = the whole R-round solve
+    corr_per_launch = int(info["total_corr"]) * (1 if info["mode"] == "graph" else R)
     achieved = BYTES_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
 
     rounds_total = world * len(sizes) * R * args.steps
@@ -159,7 +163,10 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": None,
-            "kernel": "picp_round_kernel (linearize launch)",
+            "kernel": {"graph": "picp_round_kernel (one GN round per launch)",
+                       "persistent": "picp_persistent_kernel (all GN rounds in one launch)",
+                       "block": "picp_block_kernel (all GN rounds, one block per frame)"}[info["mode"]],
+            "mode": info["mode"],
             "kernel_us": round(launch_us, 3),
             "kernel_us_event_pair": round(pair_us, 3),
             "timed_region_event_ms": round(ev_ms, 4),

@@ -157,6 +157,24 @@ int picp_triangulate(int device, const float P1[12], const float P2[12], const f
 /* Helper: P = K * inverse(T_cw)(0:3,0:4) from a camera-in-world pose (src/cam.cpp:109-112). */
 int picp_projection_matrix(const float K[9], const float T_cw[16], float P[12]);
 
+/* ---------------- descriptor matching (match_points replacement) ---------------- */
+
+/* src/my_utilities.h:70-120: for each of the n1 descriptors of set 1 (float[dim], packed) the
+ * nearest set-2 descriptor by squared L2 (best_idx, -1 if set 2 is empty), its distance and the
+ * second-nearest distance; accepted[i] = best < dist_thr && best/second < ratio_thr (the
+ * reference uses 0.2 and 0.8, src/my_utilities.h:44-46).  The accepted (i, best_idx[i]) pairs
+ * are the reference's IntPairVector.  dim in [1, 32].  Host pointers. */
+int picp_match(int device, const float* desc1, int64_t n1, const float* desc2, int64_t n2, int dim,
+               float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
+               float* second_dist, int32_t* accepted);
+/* Many independent (set 1, set 2) pairs in one launch: problem i matches desc1 rows
+ * [off1[i], off1[i+1]) against desc2 rows [off2[i], off2[i+1]); best_idx is relative to
+ * off2[i].  n_problems <= 65535. */
+int picp_match_batch(int device, int n_problems, const int64_t* off1, const int64_t* off2,
+                     const float* desc1, const float* desc2, int dim, float dist_thr,
+                     float ratio_thr, int32_t* best_idx, float* best_dist, float* second_dist,
+                     int32_t* accepted);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,8 @@ def lib():
         L.or_triangulate.argtypes = [_f32p, _f32p, _f32p, _f32p, i64, _f32p]
         L.or_projection_matrix.argtypes = [_f32p, _f32p, _f32p]
         L.or_iso_inverse.argtypes = [_f32p, _f32p]
+        L.or_match_points.argtypes = [_f32p, i64, _f32p, i64, i, f, f, _i32p, _f32p, _f32p, _i32p]
+        L.or_match_points.restype = i64
         _lib = L
     return _lib
 
@@ -197,3 +199,19 @@ def triangulate(P1, P2, uv1, uv2):
     lib().or_triangulate(_f32(P1).reshape(12), _f32(P2).reshape(12), uv1.reshape(-1),
                          uv2.reshape(-1), uv1.shape[0], out.reshape(-1))
     return out
+
+
+def match_points(d1, d2, dist_thr=0.2, ratio_thr=0.8):
+    """src/my_utilities.h:70-120 -> dict(best_idx, best_dist, second_dist, accepted)."""
+    d1 = _f32(d1)
+    d2 = _f32(d2)
+    n1 = d1.shape[0]
+    dim = d1.shape[1] if d1.ndim == 2 else d2.shape[1]
+    n2 = d2.shape[0] if d2.size else 0
+    bi = np.zeros(n1, np.int32)
+    bd = np.zeros(n1, np.float32)
+    sd = np.zeros(n1, np.float32)
+    acc = np.zeros(n1, np.int32)
+    lib().or_match_points(d1.reshape(-1), n1, d2.reshape(-1) if d2.size else np.zeros(1, np.float32), n2,
+                          dim, dist_thr, ratio_thr, bi, bd, sd, acc)
+    return {"best_idx": bi, "best_dist": bd, "second_dist": sd, "accepted": acc.astype(bool)}

@@ -503,3 +503,35 @@ void or_triangulate(const float P1[12], const float P2[12], const float* uv1, co
     xyz_out[3 * i + 2] = X4[2] * scale;
   }
 }
+
+/* match_points, src/my_utilities.h:70-120 (see picp_oracle.h) */
+int64_t or_match_points(const float* d1, int64_t n1, const float* d2, int64_t n2, int dim,
+                        float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
+                        float* second_dist, int32_t* accepted) {
+  int64_t na = 0;
+  for (int64_t i = 0; i < n1; ++i) {
+    float best = FLT_MAX, second = FLT_MAX; /* :78-79 */
+    int32_t bi = -1;
+    for (int64_t j = 0; j < n2; ++j) {      /* :83-97 */
+      float d = 0.0f;
+      for (int k = 0; k < dim; ++k) {
+        const float t = d1[i * dim + k] - d2[j * dim + k];
+        d = d + t * t;
+      }
+      if (d < best) {
+        second = best;
+        best = d;
+        bi = (int32_t)j;
+      } else if (d < second) {
+        second = d;
+      }
+    }
+    const int acc = (bi != -1 && best < dist_thr && best / second < ratio_thr); /* :100-103 */
+    best_idx[i] = bi;
+    best_dist[i] = best;
+    second_dist[i] = second;
+    accepted[i] = acc;
+    na += acc;
+  }
+  return na;
+}

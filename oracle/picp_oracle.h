@@ -106,6 +106,15 @@ void or_triangulate(const float P1[12], const float P2[12], const float* uv1, co
 /* P = K * inverse(T_camera_in_world)(0:3,0:4) as src/cam.cpp:109-112 (row-major out) */
 void or_projection_matrix(const float K[9], const float T_cw[16], float P[12]);
 
+/* match_points (src/my_utilities.h:70-120): for every descriptor of set 1 the nearest (squared
+ * L2, float, summed over the dims in order) descriptor of set 2 and the second nearest, strict
+ * '<' updates in index order; accepted iff best < dist_thr and best/second < ratio_thr
+ * (DISTANCE_THRESHOLD 0.2, RATIO_THRESHOLD 0.8, src/my_utilities.h:44-46).  best_idx = -1 when
+ * set 2 is empty.  Returns the number accepted. */
+int64_t or_match_points(const float* d1, int64_t n1, const float* d2, int64_t n2, int dim,
+                        float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
+                        float* second_dist, int32_t* accepted);
+
 /* Eigen::Isometry3f::inverse() (rigid inverse) */
 void or_iso_inverse(const float T[16], float Tinv[16]);
 

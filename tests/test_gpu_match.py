@@ -1,0 +1,66 @@
+"""GPU parity of the descriptor matcher (match_points, src/my_utilities.h:70-120) against the
+CPU oracle.  Integer/index work: best_idx, best/second distances and the accept flag must be
+BIT-IDENTICAL (both sum the squared differences in dimension order with FP contraction off)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _eq(got, ref):
+    for k in ("best_idx", "best_dist", "second_dist", "accepted"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def _sets(rng, n1, n2, dim, frac_true=0.6):
+    d2 = rng.random((n2, dim), dtype=np.float32)
+    nt = min(int(n1 * frac_true), n2)
+    d1 = rng.random((n1, dim), dtype=np.float32)
+    if nt:
+        d1[:nt] = d2[rng.choice(n2, nt, replace=False)] + rng.normal(0, 0.01, (nt, dim)).astype(np.float32)
+    return d1, d2
+
+
+@pytest.mark.parametrize("n1,n2,dim", [(1, 1, 10), (37, 300, 10), (1000, 2000, 10), (513, 257, 10),
+                                       (300, 700, 7), (200, 900, 32), (5000, 1, 10)])
+def test_match_matches_oracle(native, oracle, n1, n2, dim):
+    rng = np.random.default_rng(n1 * 31 + n2 + dim)
+    d1, d2 = _sets(rng, n1, n2, dim)
+    if n2 > 3:
+        d2[2] = d2[3]  # exact tie: lower index wins
+    _eq(native.match_points(d1, d2), oracle.match_points(d1, d2))
+
+
+def test_match_reference_data_frames(native, oracle, vo):
+    """data/: each measurement frame against the map, and consecutive frames against each other
+    (the two match_points call sites of exec/icp_test.cpp)."""
+    for k in range(0, 20):
+        f = vo.frame(k)
+        _eq(native.match_points(f["desc"], vo.world_desc), oracle.match_points(f["desc"], vo.world_desc))
+        g = vo.frame(k + 1)
+        _eq(native.match_points(f["desc"], g["desc"]), oracle.match_points(f["desc"], g["desc"]))
+
+
+def test_match_batch_ragged(native, oracle):
+    rng = np.random.default_rng(3)
+    sizes = [(0, 5), (4, 0), (300, 1000), (1, 1), (700, 50), (0, 0), (2049, 333)]
+    d1s, d2s = zip(*[_sets(rng, a, b, 10) for a, b in sizes])
+    outs = native.match_points_batch(list(d1s), list(d2s))
+    for d1, d2, got in zip(d1s, d2s, outs):
+        _eq(got, oracle.match_points(d1, d2))
+
+
+def test_match_thresholds(native, oracle):
+    rng = np.random.default_rng(11)
+    d1, d2 = _sets(rng, 800, 800, 10)
+    for dt, rt in [(0.2, 0.8), (1e9, 1.0), (0.0, 0.8), (0.05, 0.3)]:
+        _eq(native.match_points(d1, d2, dt, rt), oracle.match_points(d1, d2, dt, rt))
+
+
+def test_match_empty_and_errors(native):
+    d = np.ones((4, 10), np.float32)
+    got = native.match_points(d, np.zeros((0, 10), np.float32))
+    assert (got["best_idx"] == -1).all() and not got["accepted"].any()
+    assert len(native.match_points(np.zeros((0, 10), np.float32), d)["best_idx"]) == 0
+    with pytest.raises(Exception):
+        native.match_points(np.ones((4, 33), np.float32), np.ones((4, 33), np.float32))

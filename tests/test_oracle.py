@@ -230,3 +230,57 @@ def test_golden_vectors_regression(oracle):
         T, st = oracle.solve(p["T_init"], p["K"], 480, 640, p["world"], p["image"], p["pairs"],
                              3000.0, mode=oracle.MODE_F64, max_rounds=50, conv_eps=-1.0)
         np.testing.assert_array_equal(T, g["%s/solve_f64/T" % name])
+
+
+def _np_match(d1, d2, dist_thr=0.2, ratio_thr=0.8):
+    """Independent numpy restatement of match_points (src/my_utilities.h:70-120)."""
+    n1 = len(d1)
+    bi = np.full(n1, -1, np.int32)
+    bd = np.full(n1, np.finfo(np.float32).max, np.float32)
+    sd = np.full(n1, np.finfo(np.float32).max, np.float32)
+    for i in range(n1):
+        for j in range(len(d2)):
+            d = np.float32(0.0)
+            for k in range(d1.shape[1]):
+                t = np.float32(d1[i, k] - d2[j, k])
+                d = np.float32(d + np.float32(t * t))
+            if d < bd[i]:
+                sd[i], bd[i], bi[i] = bd[i], d, j
+            elif d < sd[i]:
+                sd[i] = d
+    with np.errstate(divide="ignore", invalid="ignore"):
+        acc = (bi != -1) & (bd < dist_thr) & (bd / sd < ratio_thr)
+    return bi, bd, sd, acc
+
+
+def test_match_points_matches_numpy_restatement(oracle):
+    rng = np.random.default_rng(7)
+    d2 = rng.random((60, 10), dtype=np.float32)
+    d1 = np.concatenate([d2[rng.permutation(60)[:25]] + rng.normal(0, 0.02, (25, 10)).astype(np.float32),
+                         rng.random((15, 10), dtype=np.float32)])
+    d2[5] = d2[6]  # an exact tie: the first index wins (strict '<')
+    got = oracle.match_points(d1, d2)
+    bi, bd, sd, acc = _np_match(d1, d2)
+    np.testing.assert_array_equal(got["best_idx"], bi)
+    np.testing.assert_array_equal(got["best_dist"], bd)
+    np.testing.assert_array_equal(got["second_dist"], sd)
+    np.testing.assert_array_equal(got["accepted"], acc)
+    assert acc.sum() >= 20
+
+
+def test_kat_match_points_on_reference_data(oracle, vo):
+    """The reference's own data/: every accepted match of frame 1 against the map is the
+    simulator's true association (noise-free descriptors)."""
+    f = vo.frame(1)
+    got = oracle.match_points(f["desc"], vo.world_desc)
+    acc = got["accepted"]
+    assert acc.sum() >= 0.9 * len(acc)
+    np.testing.assert_array_equal(vo.world_id[got["best_idx"][acc]], f["id_real"][acc])
+
+
+def test_match_points_empty_sets(oracle):
+    d = np.random.default_rng(0).random((5, 10), dtype=np.float32)
+    got = oracle.match_points(d, np.zeros((0, 10), np.float32))
+    assert (got["best_idx"] == -1).all() and not got["accepted"].any()
+    got = oracle.match_points(np.zeros((0, 10), np.float32), d)
+    assert len(got["best_idx"]) == 0
