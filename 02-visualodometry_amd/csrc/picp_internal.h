@@ -67,3 +67,61 @@ struct PicpState {
 
 static_assert(sizeof(PicpState) == 128, "PicpState must be 128 B");
 static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
+
+// ---------------------------------------------------------------------------------------
+// descriptor matching (picp_match.hip): query rows [q_off, q_off + nq) of the query
+// descriptors against reference rows [r_off, r_off + nr); best_idx is relative to r_off.
+struct MatchProblem {
+  int64_t q_off, nq, r_off, nr;
+};
+
+// ---------------------------------------------------------------------------------------
+// device-resident VO sequence (picp_vo.hip): exec/icp_test.cpp:36-136 per segment
+struct VoSegment {
+  int64_t f0;       // first frame of the segment (bootstrap pair = f0, f0+1)
+  int64_t map_off;  // first map slot of the segment
+  int64_t slot0;    // first pose / step-record slot (steps + 1 slots)
+  int32_t steps;    // PICP steps (frames f0+1 .. f0+steps are estimated)
+  int32_t pad;
+};
+
+struct VoStep {     // per pose slot; slot 0 of a segment = the bootstrap
+  int32_t n_corr;   // map correspondences of the frame (PICP input size)
+  int32_t n_in;     // inliers of the last PICP round
+  int32_t rounds;   // oneRound calls
+  int32_t n_new;    // points triangulated and appended after this frame
+  float chi_in;
+  float chi_out;
+  int32_t converged;
+  int32_t n_proj;
+};
+
+struct VoArgs {     // by value; every pointer is device memory
+  float K[9];
+  int32_t dim;
+  int32_t n_seg;
+  const int64_t* frame_off;  // n_frames + 1
+  const float2* uv;          // per observation
+  const float* desc;         // per observation, dim floats
+  const VoSegment* segs;
+  const float* boot;         // per segment: camera-in-world poses of f0 and f0+1 (2 x 16)
+  const int32_t* pm_bi;      // frame f -> f+1 matches, indexed by f's observation
+  const int32_t* pm_acc;
+  const int32_t* wm_bi;      // next frame -> map matches, indexed by the frame's observation
+  const int32_t* wm_acc;
+  float* map_xyz;            // 3 per slot
+  float* map_desc;           // dim per slot
+  int64_t* map_n;            // per segment
+  float* X;                  // PICP SoA planes, segment s at s * cap_c
+  float* Y;
+  float* Z;
+  float* U;
+  float* V;
+  int64_t cap_c;
+  PicpProblem* probs;
+  PicpState* st_in;
+  const PicpState* st_out;
+  MatchProblem* wprobs;      // next step's world-match problem of each segment
+  float* poses;              // 16 per slot, camera-in-world, column-major
+  VoStep* steps;
+};

@@ -321,68 +321,11 @@ extern "C" __global__ void picp_triangulate_kernel(const float* __restrict__ P1,
                                                    float* __restrict__ xyz) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= q) return;
-  double A[4][4], Vm[4][4];
-  const float2 a = uv1[i], b = uv2[i];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    A[0][k] = (double)a.x * (double)P1[8 + k] - (double)P1[0 + k];
-    A[1][k] = (double)a.y * (double)P1[8 + k] - (double)P1[4 + k];
-    A[2][k] = (double)b.x * (double)P2[8 + k] - (double)P2[0 + k];
-    A[3][k] = (double)b.y * (double)P2[8 + k] - (double)P2[4 + k];
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) Vm[r][c] = (r == c) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < 10; ++sweep) {
-#pragma unroll
-    for (int pq = 0; pq < 6; ++pq) {
-      const int p = (pq < 3) ? 0 : ((pq < 5) ? 1 : 2);
-      const int qq = (pq < 3) ? pq + 1 : ((pq < 5) ? pq - 1 : 3);
-      double alpha = 0.0, beta = 0.0, gamma = 0.0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        alpha += A[k][p] * A[k][p];
-        beta += A[k][qq] * A[k][qq];
-        gamma += A[k][p] * A[k][qq];
-      }
-      if (fabs(gamma) > 1e-300 && fabs(gamma) > 1e-17 * sqrt(alpha * beta)) {
-        const double zeta = (beta - alpha) / (2.0 * gamma);
-        const double t = ((zeta >= 0.0) ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double c = 1.0 / sqrt(1.0 + t * t);
-        const double s = c * t;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const double akp = A[k][p], akq = A[k][qq];
-          A[k][p] = c * akp - s * akq;
-          A[k][qq] = s * akp + c * akq;
-          const double vkp = Vm[k][p], vkq = Vm[k][qq];
-          Vm[k][p] = c * vkp - s * vkq;
-          Vm[k][qq] = s * vkp + c * vkq;
-        }
-      }
-    }
-  }
-  double nrm[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) nrm[c] = A[0][c] * A[0][c] + A[1][c] * A[1][c] + A[2][c] * A[2][c] + A[3][c] * A[3][c];
-  double best = nrm[0];
-  double v0 = Vm[0][0], v1 = Vm[1][0], v2 = Vm[2][0], v3 = Vm[3][0];
-#pragma unroll
-  for (int c = 1; c < 4; ++c) {
-    const bool take = nrm[c] < best;
-    best = take ? nrm[c] : best;
-    v0 = take ? Vm[0][c] : v0;
-    v1 = take ? Vm[1][c] : v1;
-    v2 = take ? Vm[2][c] : v2;
-    v3 = take ? Vm[3][c] : v3;
-  }
-  // points4D is float; convertPointsFromHomogeneous in float, scale 1 when |w| <= FLT_EPSILON
-  const float X4 = (float)v0, Y4 = (float)v1, Z4 = (float)v2, W4 = (float)v3;
-  const float scale = (fabsf(W4) > FLT_EPSILON) ? 1.0f / W4 : 1.0f;
-  xyz[3 * i + 0] = X4 * scale;
-  xyz[3 * i + 1] = Y4 * scale;
-  xyz[3 * i + 2] = Z4 * scale;
+  float o[3];
+  triangulate_dlt(P1, P2, uv1[i], uv2[i], o);
+  xyz[3 * i + 0] = o[0];
+  xyz[3 * i + 1] = o[1];
+  xyz[3 * i + 2] = o[2];
 }
 
 // ------------------------------- host launch wrappers -------------------------------

@@ -14,13 +14,12 @@
 #include <float.h>
 #include <stdint.h>
 
+#include "picp_internal.h"
+
 #define PICP_MATCH_BLOCK 256
 #define PICP_MATCH_TILE 256
 #define PICP_MATCH_MAXD 32
 
-struct MatchProblem {
-  int64_t q_off, nq, r_off, nr;
-};
 
 template <int D>  // D > 0: compile-time dim; D == 0: runtime dim <= PICP_MATCH_MAXD
 __global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(

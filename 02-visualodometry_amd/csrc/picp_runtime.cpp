@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "picp_c.h"
+#include "picp_host.h"
 #include "picp_internal.h"
 
 extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, const float* X,
@@ -40,9 +41,6 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
                                         PicpState* st_out);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_persistent_block(void);
-struct MatchProblem {
-  int64_t q_off, nq, r_off, nr;
-};
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
                                         const float* q_desc, const float* r_desc,
                                         const MatchProblem* probs, int dim, float dist_thr,
@@ -61,7 +59,7 @@ extern "C" hipError_t picp_launch_triangulate(hipStream_t stream, const float* P
 // ------------------------------------------------------------------------------------
 static thread_local std::string g_err;
 
-static int set_err(int code, const char* fmt, ...) {
+int picp_set_err(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -70,20 +68,7 @@ static int set_err(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
-
-#define HIP_TRY(expr)                                                                       \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess)                                                                   \
-      return set_err(e_ == hipErrorOutOfMemory ? PICP_ERR_NOMEM : PICP_ERR_DEVICE,          \
-                     "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,       \
-                     __LINE__);                                                             \
-  } while (0)
-
-#define CHECK_ARG(cond, msg)                                                                \
-  do {                                                                                      \
-    if (!(cond)) return set_err(PICP_ERR_ARG, "%s", msg);                                   \
-  } while (0)
+#define set_err picp_set_err
 
 extern "C" const char* picp_last_error(void) { return g_err.c_str(); }
 extern "C" int picp_abi_version(void) { return PICP_ABI_VERSION; }

@@ -1,0 +1,410 @@
+// picp_vo_runtime.cpp -- host side of the device-resident VO sequence (picp_vo.hip), C-ABI in
+// include/picp_c.h (picp_vo_*).
+//
+// A handle owns one packed observation sequence in HBM (frame offsets, uv, descriptors) and,
+// after picp_vo_set_segments, everything a run needs: per-segment maps, the PICP SoA planes,
+// problem tables and states, match outputs, poses and step records.  A run is
+//   1 (or ceil(frames/65535)) launch(es) matching every frame f against f+1,
+//   1 bootstrap append, then per step: world match, gather, picp_block_kernel, append,
+// enqueued back to back on the handle's stream and captured once into a hipGraph that is
+// replayed by every later run.  No host round trip inside a run; no host fallback.
+#include <hip/hip_runtime.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "picp_c.h"
+#include "picp_host.h"
+#include "picp_internal.h"
+
+extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
+                                        const float* q_desc, const float* r_desc,
+                                        const MatchProblem* probs, int dim, float dist_thr,
+                                        float ratio_thr, int32_t* best_idx, float* best_dist,
+                                        float* second_dist, int32_t* accepted);
+extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
+                                        const float* Y, const float* Z, const float* U,
+                                        const float* V, const PicpArgs* args,
+                                        const PicpProblem* probs, const PicpState* st_in,
+                                        PicpState* st_out);
+extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
+extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
+
+static_assert(sizeof(picp_vo_step) == sizeof(VoStep), "picp_vo_step must mirror VoStep");
+
+#define VO_MATCH_DIST 0.2f   // DISTANCE_THRESHOLD, src/my_utilities.h:44
+#define VO_MATCH_RATIO 0.8f  // RATIO_THRESHOLD, src/my_utilities.h:46
+#define VO_MAX_GRID_Y 65535
+
+struct picp_vo {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int rows = 0, cols = 0, dim = 0;
+  float K[9];
+  int64_t n_frames = 0, n_obs = 0, max_obs = 0;
+  std::vector<int64_t> frame_off;
+  // sequence, resident
+  int64_t* frame_off_d = nullptr;
+  float2* uv_d = nullptr;
+  float* desc_d = nullptr;
+  int32_t *pm_bi = nullptr, *pm_acc = nullptr, *wm_bi = nullptr, *wm_acc = nullptr;
+  float *pm_bd = nullptr, *pm_sd = nullptr, *wm_bd = nullptr, *wm_sd = nullptr;
+  // segments
+  int n_seg = 0, max_steps = 0, npt = 1;
+  int64_t map_slots = 0, n_slots = 0, cap_c = 0;
+  std::vector<VoSegment> segs;
+  std::vector<MatchProblem> pprobs;
+  void* seg_mem = nullptr;  // one allocation for everything sized by the segments
+  PicpArgs pargs;
+  VoArgs vargs;
+  MatchProblem* pprobs_d = nullptr;
+  MatchProblem* wprobs_d = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool use_graph = true;
+};
+
+static void vo_free_segments(picp_vo* h) {
+  if (h->exec) hipGraphExecDestroy(h->exec);
+  if (h->graph) hipGraphDestroy(h->graph);
+  h->exec = nullptr;
+  h->graph = nullptr;
+  if (h->seg_mem) hipFree(h->seg_mem);
+  h->seg_mem = nullptr;
+  h->n_seg = 0;
+}
+
+extern "C" int picp_vo_destroy(picp_vo_t* h) {
+  if (!h) return PICP_OK;
+  if (h->stream) hipStreamSynchronize(h->stream);
+  vo_free_segments(h);
+  void* bufs[] = {h->frame_off_d, h->uv_d, h->desc_d, h->pm_bi, h->pm_acc, h->wm_bi, h->wm_acc,
+                  h->pm_bd, h->pm_sd, h->wm_bd, h->wm_sd};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (h->ev0) hipEventDestroy(h->ev0);
+  if (h->ev1) hipEventDestroy(h->ev1);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, const float K[9],
+                              int64_t n_frames, const int64_t* frame_off, const float* uv,
+                              const float* desc, int dim) {
+  CHECK_ARG(out, "picp_vo_create: null output");
+  *out = nullptr;
+  CHECK_ARG(K && frame_off && rows > 0 && cols > 0, "picp_vo_create: bad camera or frame table");
+  CHECK_ARG(n_frames >= 2, "picp_vo_create: need at least two frames");
+  CHECK_ARG(dim >= 1 && dim <= 32, "picp_vo_create: dim must be in [1, 32]");
+  CHECK_ARG(frame_off[0] == 0, "picp_vo_create: frame_off[0] must be 0");
+  int64_t mx = 0;
+  for (int64_t f = 0; f < n_frames; ++f) {
+    CHECK_ARG(frame_off[f + 1] >= frame_off[f], "picp_vo_create: frame_off must be non-decreasing");
+    mx = std::max(mx, frame_off[f + 1] - frame_off[f]);
+  }
+  CHECK_ARG(mx <= (1 << 30), "picp_vo_create: frame too large");
+  const int64_t n_obs = frame_off[n_frames];
+  CHECK_ARG(n_obs == 0 || (uv && desc), "picp_vo_create: null observation arrays");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  CHECK_ARG(device >= 0 && device < ndev, "picp_vo_create: no such HIP device");
+  HIP_TRY(hipSetDevice(device));
+  picp_vo* h = new picp_vo();
+  h->device = device;
+  h->rows = rows;
+  h->cols = cols;
+  h->dim = dim;
+  memcpy(h->K, K, sizeof(h->K));
+  h->n_frames = n_frames;
+  h->n_obs = n_obs;
+  h->max_obs = mx;
+  h->frame_off.assign(frame_off, frame_off + n_frames + 1);
+  if (const char* e = getenv("PICP_VO_GRAPH")) h->use_graph = atoi(e) != 0;
+  const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
+#define VO_TRY(expr)              \
+  do {                            \
+    int rc_ = (expr);             \
+    if (rc_ != PICP_OK) {         \
+      picp_vo_destroy(h);         \
+      return rc_;                 \
+    }                             \
+  } while (0)
+  auto alloc = [&](void** p, size_t bytes) -> int {
+    HIP_TRY(hipMalloc(p, bytes));
+    return PICP_OK;
+  };
+  VO_TRY([&]() -> int {
+    HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&h->ev0));
+    HIP_TRY(hipEventCreate(&h->ev1));
+    return PICP_OK;
+  }());
+  VO_TRY(alloc((void**)&h->frame_off_d, (size_t)(n_frames + 1) * sizeof(int64_t)));
+  VO_TRY(alloc((void**)&h->uv_d, no * sizeof(float2)));
+  VO_TRY(alloc((void**)&h->desc_d, no * dim * sizeof(float)));
+  VO_TRY(alloc((void**)&h->pm_bi, no * 4));
+  VO_TRY(alloc((void**)&h->pm_acc, no * 4));
+  VO_TRY(alloc((void**)&h->wm_bi, no * 4));
+  VO_TRY(alloc((void**)&h->wm_acc, no * 4));
+  VO_TRY(alloc((void**)&h->pm_bd, no * 4));
+  VO_TRY(alloc((void**)&h->pm_sd, no * 4));
+  VO_TRY(alloc((void**)&h->wm_bd, no * 4));
+  VO_TRY(alloc((void**)&h->wm_sd, no * 4));
+  VO_TRY([&]() -> int {
+    HIP_TRY(hipMemcpy(h->frame_off_d, frame_off, (size_t)(n_frames + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (n_obs) {
+      HIP_TRY(hipMemcpy(h->uv_d, uv, (size_t)n_obs * sizeof(float2), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(h->desc_d, desc, (size_t)n_obs * dim * sizeof(float), hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemset(h->wm_acc, 0, no * 4));
+    return PICP_OK;
+  }());
+#undef VO_TRY
+  *out = h;
+  return PICP_OK;
+}
+
+static int64_t frame_n(const picp_vo* h, int64_t f) { return h->frame_off[f + 1] - h->frame_off[f]; }
+
+extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* first,
+                                    const int32_t* steps, const float* boot_poses,
+                                    const picp_params* prm) {
+  CHECK_ARG(h && first && steps && boot_poses && prm, "picp_vo_set_segments: null argument");
+  CHECK_ARG(n_seg >= 1 && n_seg <= VO_MAX_GRID_Y, "picp_vo_set_segments: n_seg must be in [1, 65535]");
+  CHECK_ARG(prm->max_rounds >= 0 && prm->max_rounds <= 100000, "params.max_rounds out of range");
+  CHECK_ARG(!(prm->threshold != prm->threshold), "params.threshold is NaN");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  vo_free_segments(h);
+  std::vector<VoSegment> segs((size_t)n_seg);
+  std::vector<char> is_curr((size_t)h->n_frames, 0);
+  int64_t map_slots = 0, n_slots = 0;
+  int max_steps = 0;
+  for (int s = 0; s < n_seg; ++s) {
+    CHECK_ARG(steps[s] >= 1 && first[s] >= 0 && first[s] + steps[s] < h->n_frames,
+              "picp_vo_set_segments: segment out of range (needs frames first .. first+steps, steps >= 1)");
+    VoSegment& G = segs[s];
+    G.f0 = first[s];
+    G.steps = steps[s];
+    G.pad = 0;
+    G.map_off = map_slots;
+    G.slot0 = n_slots;
+    int64_t cap = frame_n(h, G.f0);  // bootstrap adds <= |frame f0|, step t adds <= |frame f0+t|
+    for (int t = 0; t < G.steps; ++t) cap += frame_n(h, G.f0 + t);
+    map_slots += std::max<int64_t>(cap, 1);
+    n_slots += G.steps + 1;
+    max_steps = std::max(max_steps, (int)G.steps);
+    for (int64_t f = G.f0; f < G.f0 + G.steps; ++f) is_curr[f] = 1;
+  }
+  std::vector<MatchProblem> pprobs;
+  for (int64_t f = 0; f + 1 < h->n_frames; ++f)
+    if (is_curr[f] && frame_n(h, f) > 0)
+      pprobs.push_back(MatchProblem{h->frame_off[f], frame_n(h, f), h->frame_off[f + 1], frame_n(h, f + 1)});
+  int64_t cap_c = (std::max<int64_t>(h->max_obs, 1) + 3) / 4 * 4;
+  int npt = 1;
+  while (npt < 8 && (int64_t)npt * 512 < h->max_obs) npt *= 2;
+
+  // one allocation for everything sized by the segments
+  struct Part { size_t off, bytes; };
+  size_t total = 0;
+  auto part = [&](size_t bytes) { Part p{total, bytes}; total += (bytes + 255) / 256 * 256; return p; };
+  const Part p_segs = part(segs.size() * sizeof(VoSegment));
+  const Part p_boot = part((size_t)n_seg * 32 * sizeof(float));
+  const Part p_mxyz = part((size_t)map_slots * 3 * sizeof(float));
+  const Part p_mdesc = part((size_t)map_slots * h->dim * sizeof(float));
+  const Part p_mn = part((size_t)n_seg * sizeof(int64_t));
+  const Part p_planes = part((size_t)5 * n_seg * cap_c * sizeof(float));
+  const Part p_probs = part((size_t)n_seg * sizeof(PicpProblem));
+  const Part p_stin = part((size_t)n_seg * sizeof(PicpState));
+  const Part p_stout = part((size_t)n_seg * sizeof(PicpState));
+  const Part p_wprobs = part((size_t)n_seg * sizeof(MatchProblem));
+  const Part p_pprobs = part(std::max<size_t>(pprobs.size(), 1) * sizeof(MatchProblem));
+  const Part p_poses = part((size_t)n_slots * 16 * sizeof(float));
+  const Part p_steps = part((size_t)n_slots * sizeof(VoStep));
+  HIP_TRY(hipMalloc(&h->seg_mem, total));
+  char* m = (char*)h->seg_mem;
+  h->segs = segs;
+  h->pprobs = pprobs;
+  h->n_seg = n_seg;
+  h->max_steps = max_steps;
+  h->npt = npt;
+  h->map_slots = map_slots;
+  h->n_slots = n_slots;
+  h->cap_c = cap_c;
+  HIP_TRY(hipMemcpy(m + p_segs.off, segs.data(), p_segs.bytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(m + p_boot.off, boot_poses, p_boot.bytes, hipMemcpyHostToDevice));
+  if (!pprobs.empty()) HIP_TRY(hipMemcpy(m + p_pprobs.off, pprobs.data(), p_pprobs.bytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(m + p_mn.off, 0, p_mn.bytes));
+  HIP_TRY(hipMemset(m + p_steps.off, 0, p_steps.bytes));
+  HIP_TRY(hipMemset(m + p_poses.off, 0, p_poses.bytes));
+  HIP_TRY(hipMemset(m + p_planes.off, 0, p_planes.bytes));
+
+  PicpArgs& A = h->pargs;
+  memset(&A, 0, sizeof(A));
+  memcpy(A.K, h->K, sizeof(A.K));
+  A.maxx = (float)(h->cols - 1);
+  A.maxy = (float)(h->rows - 1);
+  A.threshold = prm->threshold;
+  A.damping = prm->damping;
+  A.conv_eps = prm->conv_eps;
+  A.min_inliers = prm->min_inliers;
+  A.keep_outliers = prm->keep_outliers ? 1 : 0;
+  A.max_rounds = prm->max_rounds;
+  A.uniform = 0;
+
+  VoArgs& V = h->vargs;
+  memset(&V, 0, sizeof(V));
+  memcpy(V.K, h->K, sizeof(V.K));
+  V.dim = h->dim;
+  V.n_seg = n_seg;
+  V.frame_off = h->frame_off_d;
+  V.uv = h->uv_d;
+  V.desc = h->desc_d;
+  V.segs = (const VoSegment*)(m + p_segs.off);
+  V.boot = (const float*)(m + p_boot.off);
+  V.pm_bi = h->pm_bi;
+  V.pm_acc = h->pm_acc;
+  V.wm_bi = h->wm_bi;
+  V.wm_acc = h->wm_acc;
+  V.map_xyz = (float*)(m + p_mxyz.off);
+  V.map_desc = (float*)(m + p_mdesc.off);
+  V.map_n = (int64_t*)(m + p_mn.off);
+  float* planes = (float*)(m + p_planes.off);
+  const size_t plane = (size_t)n_seg * cap_c;
+  V.X = planes;
+  V.Y = planes + plane;
+  V.Z = planes + 2 * plane;
+  V.U = planes + 3 * plane;
+  V.V = planes + 4 * plane;
+  V.cap_c = cap_c;
+  V.probs = (PicpProblem*)(m + p_probs.off);
+  V.st_in = (PicpState*)(m + p_stin.off);
+  V.st_out = (const PicpState*)(m + p_stout.off);
+  V.wprobs = (MatchProblem*)(m + p_wprobs.off);
+  V.poses = (float*)(m + p_poses.off);
+  V.steps = (VoStep*)(m + p_steps.off);
+  h->wprobs_d = V.wprobs;
+  h->pprobs_d = (MatchProblem*)(m + p_pprobs.off);
+  return PICP_OK;
+}
+
+// the whole sequence, back to back on the handle's stream
+static hipError_t vo_enqueue(picp_vo* h) {
+  hipError_t e = hipSuccess;
+  for (size_t p0 = 0; p0 < h->pprobs.size() && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
+    const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, h->pprobs.size() - p0);
+    e = picp_launch_match(h->stream, np, h->max_obs, h->desc_d, h->desc_d, h->pprobs_d + p0, h->dim,
+                          VO_MATCH_DIST, VO_MATCH_RATIO, h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc);
+  }
+  if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
+  const VoArgs& V = h->vargs;
+  for (int t = 0; t < h->max_steps && e == hipSuccess; ++t) {
+    e = picp_launch_match(h->stream, h->n_seg, h->max_obs, h->desc_d, V.map_desc, h->wprobs_d, h->dim,
+                          VO_MATCH_DIST, VO_MATCH_RATIO, h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc);
+    if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
+    if (e == hipSuccess)
+      e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,
+                            V.st_in, (PicpState*)V.st_out);
+    if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &V, t);
+  }
+  return e;
+}
+
+static int vo_launch(picp_vo* h) {
+  CHECK_ARG(h && h->n_seg > 0, "picp_vo: no segments set");
+  HIP_TRY(hipSetDevice(h->device));
+  if (!h->use_graph) {
+    HIP_TRY(vo_enqueue(h));
+    return PICP_OK;
+  }
+  if (!h->exec) {
+    HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = vo_enqueue(h);
+    hipGraph_t g = nullptr;
+    hipError_t e2 = hipStreamEndCapture(h->stream, &g);
+    if (e != hipSuccess || e2 != hipSuccess) {
+      if (g) hipGraphDestroy(g);
+      return picp_set_err(PICP_ERR_DEVICE, "picp_vo: graph capture failed: %s",
+                          hipGetErrorString(e != hipSuccess ? e : e2));
+    }
+    h->graph = g;
+    HIP_TRY(hipGraphInstantiate(&h->exec, g, nullptr, nullptr, 0));
+  }
+  HIP_TRY(hipGraphLaunch(h->exec, h->stream));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_run_async(picp_vo_t* h) { return vo_launch(h); }
+
+extern "C" int picp_vo_sync(picp_vo_t* h) {
+  CHECK_ARG(h, "picp_vo_sync: null handle");
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_run(picp_vo_t* h) {
+  int rc = vo_launch(h);
+  if (rc != PICP_OK) return rc;
+  return picp_vo_sync(h);
+}
+
+extern "C" int picp_vo_time(picp_vo_t* h, int reps, float* ms_per_run) {
+  CHECK_ARG(h && ms_per_run && reps >= 1, "picp_vo_time: bad argument");
+  int rc = vo_launch(h);  // warm (and capture)
+  if (rc != PICP_OK) return rc;
+  HIP_TRY(hipEventRecord(h->ev0, h->stream));
+  for (int r = 0; r < reps; ++r) {
+    rc = vo_launch(h);
+    if (rc != PICP_OK) return rc;
+  }
+  HIP_TRY(hipEventRecord(h->ev1, h->stream));
+  HIP_TRY(hipEventSynchronize(h->ev1));
+  float ms = 0.0f;
+  HIP_TRY(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  *ms_per_run = ms / reps;
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_get_poses(picp_vo_t* h, float* poses) {
+  CHECK_ARG(h && poses && h->n_seg > 0, "picp_vo_get_poses: bad argument");
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy(poses, h->vargs.poses, (size_t)h->n_slots * 16 * sizeof(float), hipMemcpyDeviceToHost));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_get_steps(picp_vo_t* h, picp_vo_step* steps) {
+  CHECK_ARG(h && steps && h->n_seg > 0, "picp_vo_get_steps: bad argument");
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy(steps, h->vargs.steps, (size_t)h->n_slots * sizeof(VoStep), hipMemcpyDeviceToHost));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_get_map(picp_vo_t* h, int seg, int64_t cap, float* xyz, float* desc, int64_t* n) {
+  CHECK_ARG(h && n && h->n_seg > 0 && seg >= 0 && seg < h->n_seg, "picp_vo_get_map: bad argument");
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  int64_t mn = 0;
+  HIP_TRY(hipMemcpy(&mn, h->vargs.map_n + seg, sizeof(int64_t), hipMemcpyDeviceToHost));
+  *n = mn;
+  const int64_t k = std::min(mn, std::max<int64_t>(cap, 0));
+  const int64_t off = h->segs[seg].map_off;
+  if (xyz && k)
+    HIP_TRY(hipMemcpy(xyz, h->vargs.map_xyz + 3 * off, (size_t)k * 3 * sizeof(float), hipMemcpyDeviceToHost));
+  if (desc && k)
+    HIP_TRY(hipMemcpy(desc, h->vargs.map_desc + off * h->dim, (size_t)k * h->dim * sizeof(float),
+                      hipMemcpyDeviceToHost));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_info(picp_vo_t* h, int64_t* n_obs, int64_t* n_slots, int64_t* map_slots, int* npt) {
+  CHECK_ARG(h, "picp_vo_info: null handle");
+  if (n_obs) *n_obs = h->n_obs;
+  if (n_slots) *n_slots = h->n_slots;
+  if (map_slots) *map_slots = h->map_slots;
+  if (npt) *npt = h->npt;
+  return PICP_OK;
+}

@@ -41,6 +41,9 @@ EXPORTED = [
     "picp_batch_get_poses", "picp_batch_get_stats", "picp_batch_solve",
     "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_info",
     "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
+    "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async",
+    "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
+    "picp_vo_info",
 ]
 
 
@@ -58,6 +61,12 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class VOStep(ctypes.Structure):
+    _fields_ = [("n_corr", ctypes.c_int32), ("n_in", ctypes.c_int32), ("rounds", ctypes.c_int32),
+                ("n_new", ctypes.c_int32), ("chi_in", ctypes.c_float), ("chi_out", ctypes.c_float),
+                ("converged", ctypes.c_int32), ("n_projected", ctypes.c_int32)]
 
 
 class Params(ctypes.Structure):
@@ -120,6 +129,17 @@ def lib():
                         ctypes.POINTER(ctypes.c_int32)], i),
         "picp_match_batch": ([i, i, ctypes.POINTER(i64), ctypes.POINTER(i64), fp, fp, i, f, f,
                               ctypes.POINTER(ctypes.c_int32), fp, fp, ctypes.POINTER(ctypes.c_int32)], i),
+        "picp_vo_create": ([ctypes.POINTER(vp), i, i, i, fp, i64, ctypes.POINTER(i64), fp, fp, i], i),
+        "picp_vo_destroy": ([vp], i),
+        "picp_vo_set_segments": ([vp, i, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_int32), fp, pp], i),
+        "picp_vo_run": ([vp], i),
+        "picp_vo_run_async": ([vp], i),
+        "picp_vo_sync": ([vp], i),
+        "picp_vo_get_poses": ([vp, fp], i),
+        "picp_vo_get_steps": ([vp, ctypes.POINTER(VOStep)], i),
+        "picp_vo_get_map": ([vp, i, i64, fp, fp, ctypes.POINTER(i64)], i),
+        "picp_vo_time": ([vp, i, fp], i),
+        "picp_vo_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i)], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -396,3 +416,92 @@ def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, devi
     return [{"best_idx": bi[o1[i]:o1[i + 1]], "best_dist": bd[o1[i]:o1[i + 1]],
              "second_dist": sd[o1[i]:o1[i + 1]], "accepted": acc[o1[i]:o1[i + 1]].astype(bool)}
             for i in range(len(desc1_list))]
+
+
+class VOSequence:
+    """Device-resident VO over a packed observation sequence (C-ABI picp_vo_*): the reference's
+    per-frame loop (exec/icp_test.cpp:61-136) run on the GPU for independent segments in
+    lockstep.  Poses are camera-in-world 4x4 (numpy row/col)."""
+
+    def __init__(self, frame_off, uv, desc, device=0, rows=480, cols=640, K=K_REF):
+        self.frame_off = np.ascontiguousarray(frame_off, np.int64)
+        uv = _f32(uv, (-1,))
+        desc = np.ascontiguousarray(desc, np.float32)
+        self.dim = desc.shape[1]
+        self.n_frames = len(self.frame_off) - 1
+        self._h = ctypes.c_void_p()
+        _check(lib().picp_vo_create(ctypes.byref(self._h), device, rows, cols, _fptr(k_to_c(K)),
+                                    self.n_frames, self.frame_off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                    _fptr(uv), _fptr(desc.reshape(-1)), self.dim))
+        self.first = self.steps = None
+
+    def close(self):
+        if self._h:
+            lib().picp_vo_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_segments(self, first, steps, boot_poses, threshold=3000.0, **params):
+        """boot_poses: (n_seg, 2, 4, 4) camera-in-world poses of frames first and first+1."""
+        self.first = np.ascontiguousarray(first, np.int64)
+        self.steps = np.ascontiguousarray(steps, np.int32)
+        B = np.asarray(boot_poses, np.float32).reshape(len(self.first), 2, 4, 4)
+        flat = np.ascontiguousarray(np.transpose(B, (0, 1, 3, 2)).reshape(-1))
+        p = default_params(threshold=threshold, **params)
+        _check(lib().picp_vo_set_segments(self._h, len(self.first),
+                                          self.first.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                          self.steps.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                          _fptr(flat), ctypes.byref(p)))
+
+    def run(self):
+        _check(lib().picp_vo_run(self._h))
+
+    def time(self, reps):
+        ms = ctypes.c_float()
+        _check(lib().picp_vo_time(self._h, reps, ctypes.byref(ms)))
+        return ms.value
+
+    def info(self):
+        n_obs, n_slots, map_slots, npt = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+        _check(lib().picp_vo_info(self._h, ctypes.byref(n_obs), ctypes.byref(n_slots), ctypes.byref(map_slots),
+                                  ctypes.byref(npt)))
+        return {"n_obs": n_obs.value, "n_slots": n_slots.value, "map_slots": map_slots.value, "npt": npt.value}
+
+    def _split(self, flat):
+        out, o = [], 0
+        for st in self.steps:
+            out.append(flat[o:o + st + 1])
+            o += st + 1
+        return out
+
+    def poses(self):
+        """list over segments of (steps+1, 4, 4) camera-in-world poses ([0] = bootstrap pose)."""
+        n = int((self.steps + 1).sum())
+        out = np.zeros(16 * n, np.float32)
+        _check(lib().picp_vo_get_poses(self._h, _fptr(out)))
+        return self._split(np.transpose(out.reshape(n, 4, 4), (0, 2, 1)).copy())
+
+    def step_records(self):
+        """list over segments of dicts of arrays (steps+1 entries; entry 0 = bootstrap)."""
+        n = int((self.steps + 1).sum())
+        arr = (VOStep * n)()
+        _check(lib().picp_vo_get_steps(self._h, arr))
+        recs = {k: np.array([getattr(a, k) for a in arr]) for k, _ in VOStep._fields_}
+        out, o = [], 0
+        for st in self.steps:
+            out.append({k: v[o:o + st + 1] for k, v in recs.items()})
+            o += st + 1
+        return out
+
+    def map(self, seg):
+        n = ctypes.c_int64()
+        _check(lib().picp_vo_get_map(self._h, seg, 0, None, None, ctypes.byref(n)))
+        xyz = np.zeros(max(n.value, 1) * 3, np.float32)
+        desc = np.zeros(max(n.value, 1) * self.dim, np.float32)
+        _check(lib().picp_vo_get_map(self._h, seg, n.value, _fptr(xyz), _fptr(desc), ctypes.byref(n)))
+        return xyz[:3 * n.value].reshape(-1, 3), desc[:self.dim * n.value].reshape(-1, self.dim)

@@ -32,6 +32,7 @@ class VOData:
         self.K = d["K"]
         self.rows = int(d["rows"])
         self.ref_errors = d["ref_errors"] if "ref_errors" in d else None
+        self.ref_map_ids = d["ref_map_ids"] if "ref_map_ids" in d else None
         self.cols = int(d["cols"])
         self.n_frames = self.gt_pose.shape[0]
         self._id2row = {int(i): r for r, i in enumerate(self.world_id)}
@@ -70,3 +71,15 @@ class VOData:
         f = self.frame(k)
         pairs = [(i, self._id2row[int(r)]) for i, r in enumerate(f["id_real"]) if int(r) in self._id2row]
         return np.array(pairs, np.int32).reshape(-1, 2)
+
+    def packed(self):
+        """The 121 frames packed for the VO sequence APIs: (frame_off int64, uv, desc)."""
+        order = np.lexsort((self.meas_id, self.meas_frame))
+        off = np.zeros(self.n_frames + 1, np.int64)
+        off[1:] = np.cumsum(np.bincount(self.meas_frame, minlength=self.n_frames))
+        return off, np.ascontiguousarray(self.meas_uv[order]), np.ascontiguousarray(self.meas_desc[order])
+
+    def map_ids(self, map_desc):
+        """id_real of map points by exact descriptor identity with world.dat (noise-free data)."""
+        lut = {self.world_desc[r].tobytes(): int(self.world_id[r]) for r in range(len(self.world_id))}
+        return np.array([lut.get(np.asarray(d, np.float32).tobytes(), -1) for d in map_desc], np.int64)

@@ -175,6 +175,52 @@ int picp_match_batch(int device, int n_problems, const int64_t* off1, const int6
                      float ratio_thr, int32_t* best_idx, float* best_dist, float* second_dist,
                      int32_t* accepted);
 
+/* ---------------- device-resident VO sequence (exec/icp_test.cpp:36-136) ---------------- */
+
+/* The reference's per-frame loop (match next<->map, PICP from the previous pose, match
+ * curr<->next, add_new_world_points, triangulate, append) run entirely on the GPU over
+ * independent SEGMENTS of a sequence that advance in lockstep.  Segment s
+ * covers frames first[s] .. first[s]+steps[s]: it bootstraps its map by triangulating the
+ * matches of its first two frames with the given camera-in-world poses (a stand-in for
+ * computeEssentialAndRecoverPose, exec/icp_test.cpp:44-58), then estimates frames
+ * first[s]+1 .. first[s]+steps[s].  Matching uses DISTANCE_THRESHOLD 0.2 / RATIO 0.8. */
+typedef struct picp_vo picp_vo_t;
+
+/* One pose slot's record; slot 0 of a segment is its bootstrap (only n_new set). */
+typedef struct {
+  int32_t n_corr;   /* map correspondences of the frame (size of the PICP problem) */
+  int32_t n_in;     /* numInliers() after the last round */
+  int32_t rounds;   /* oneRound calls */
+  int32_t n_new;    /* points triangulated into the map after this frame */
+  float chi_in;
+  float chi_out;
+  int32_t converged;
+  int32_t n_projected;
+} picp_vo_step;
+
+/* Upload (copy) a packed sequence: frame f = observations [frame_off[f], frame_off[f+1]) of
+ * uv (float2, meas-*.dat "point" u v) and desc (float[dim]); frame_off[0] == 0. */
+int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, const float K[9],
+                   int64_t n_frames, const int64_t* frame_off, const float* uv,
+                   const float* desc, int dim);
+int picp_vo_destroy(picp_vo_t* h);
+/* boot_poses: per segment two column-major 4x4 camera-in-world poses (frames first, first+1).
+ * params: threshold (icp_test: 3000), damping, min_inliers, keep_outliers, max_rounds,
+ * conv_eps of the per-frame PICP loop. */
+int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* first, const int32_t* steps,
+                         const float* boot_poses, const picp_params* params);
+int picp_vo_run(picp_vo_t* h);        /* enqueue the whole sequence and wait */
+int picp_vo_run_async(picp_vo_t* h);
+int picp_vo_sync(picp_vo_t* h);
+/* poses: sum(steps+1) camera-in-world 4x4 (segment-major; slot 0 = the bootstrap pose) */
+int picp_vo_get_poses(picp_vo_t* h, float* poses);
+int picp_vo_get_steps(picp_vo_t* h, picp_vo_step* steps);
+/* segment map: *n = its size; the first min(n, cap) points are copied to xyz / desc (nullable) */
+int picp_vo_get_map(picp_vo_t* h, int seg, int64_t cap, float* xyz, float* desc, int64_t* n);
+/* mean device time of `reps` back-to-back runs (HIP events on the handle's stream) */
+int picp_vo_time(picp_vo_t* h, int reps, float* ms_per_run);
+int picp_vo_info(picp_vo_t* h, int64_t* n_obs, int64_t* n_slots, int64_t* map_slots, int* npt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,10 @@ def lib():
         L.or_iso_inverse.argtypes = [_f32p, _f32p]
         L.or_match_points.argtypes = [_f32p, i64, _f32p, i64, i, f, f, _i32p, _f32p, _f32p, _i32p]
         L.or_match_points.restype = i64
+        L.or_vo_segment.argtypes = [_f32p, i, i, np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS"),
+                                    _f32p, _f32p, i, i64, i, _f32p, _f32p, f, i, i, f, _f32p, _i32p,
+                                    _i32p, _i32p, _i32p, i64, _f32p, _f32p]
+        L.or_vo_segment.restype = i64
         _lib = L
     return _lib
 
@@ -215,3 +219,30 @@ def match_points(d1, d2, dist_thr=0.2, ratio_thr=0.8):
     lib().or_match_points(d1.reshape(-1), n1, d2.reshape(-1) if d2.size else np.zeros(1, np.float32), n2,
                           dim, dist_thr, ratio_thr, bi, bd, sd, acc)
     return {"best_idx": bi, "best_dist": bd, "second_dist": sd, "accepted": acc.astype(bool)}
+
+
+def vo_segment(K, rows, cols, frame_off, uv, desc, f0, steps, T0, T1, threshold=3000.0,
+               mode=MODE_F64, max_rounds=50, conv_eps=1e-5, map_cap=None):
+    """exec/icp_test.cpp:36-136 over frames [f0, f0+steps] (see picp_oracle.h or_vo_segment).
+    T0/T1: camera-in-world bootstrap poses (4x4).  Returns dict(poses (steps+1,4,4) camera-in-world,
+    n_corr, n_in, rounds, n_new, map_xyz, map_desc)."""
+    frame_off = np.ascontiguousarray(frame_off, np.int64)
+    desc = _f32(desc)
+    dim = desc.shape[1]
+    if map_cap is None:
+        map_cap = int(frame_off[f0 + steps + 1] - frame_off[f0])
+    poses = np.zeros((steps + 1) * 16, np.float32)
+    n_corr = np.zeros(max(steps, 1), np.int32)
+    n_in = np.zeros(max(steps, 1), np.int32)
+    rounds = np.zeros(max(steps, 1), np.int32)
+    n_new = np.zeros(steps + 1, np.int32)
+    mx = np.zeros(max(map_cap, 1) * 3, np.float32)
+    md = np.zeros(max(map_cap, 1) * dim, np.float32)
+    n = lib().or_vo_segment(_k9(K), rows, cols, frame_off, _f32(uv).reshape(-1), desc.reshape(-1), dim,
+                            int(f0), int(steps), _pose16(T0), _pose16(T1), threshold, mode, max_rounds,
+                            conv_eps, poses, n_corr, n_in, rounds, n_new, map_cap, mx, md)
+    if n < 0:
+        raise RuntimeError("or_vo_segment: map capacity exceeded")
+    return {"poses": np.stack([_pose44(poses[16 * k:16 * k + 16]) for k in range(steps + 1)]),
+            "n_corr": n_corr[:steps], "n_in": n_in[:steps], "rounds": rounds[:steps], "n_new": n_new,
+            "map_xyz": mx[:3 * n].reshape(-1, 3), "map_desc": md[:dim * n].reshape(-1, dim)}

@@ -17,6 +17,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define TM(T, i, j) ((T)[(j) * 4 + (i)]) /* column-major 4x4 */
@@ -534,4 +535,99 @@ int64_t or_match_points(const float* d1, int64_t n1, const float* d2, int64_t n2
     na += acc;
   }
   return na;
+}
+
+/* ---------------------------------------------------------------------------------------
+ * VO segment loop, exec/icp_test.cpp:36-136 (see picp_oracle.h)
+ * ------------------------------------------------------------------------------------- */
+static int64_t vo_append(const float K[9], const float Tprev[16], const float Test[16],
+                         const float* uv_a, const float* uv_b, const float* desc_a, int dim,
+                         const int32_t* ia, const int32_t* ib, int64_t q, int64_t map_n,
+                         int64_t map_cap, float* map_xyz, float* map_desc) {
+  if (q == 0) return map_n;
+  if (map_n + q > map_cap) return -1;
+  float P1[12], P2[12];
+  or_projection_matrix(K, Tprev, P1); /* src/cam.cpp:109-112 */
+  or_projection_matrix(K, Test, P2);
+  float* a = (float*)malloc((size_t)q * 2 * sizeof(float));
+  float* b = (float*)malloc((size_t)q * 2 * sizeof(float));
+  for (int64_t k = 0; k < q; ++k) {
+    a[2 * k] = uv_a[2 * ia[k]];
+    a[2 * k + 1] = uv_a[2 * ia[k] + 1];
+    b[2 * k] = uv_b[2 * ib[k]];
+    b[2 * k + 1] = uv_b[2 * ib[k] + 1];
+    memcpy(map_desc + (map_n + k) * dim, desc_a + (int64_t)ia[k] * dim, (size_t)dim * sizeof(float));
+  }
+  or_triangulate(P1, P2, a, b, q, map_xyz + 3 * map_n); /* src/cam.cpp:115-139 */
+  free(a);
+  free(b);
+  return map_n + q;
+}
+
+int64_t or_vo_segment(const float K[9], int rows, int cols, const int64_t* frame_off,
+                      const float* uv, const float* desc, int dim, int64_t f0, int steps,
+                      const float T0[16], const float T1[16], float threshold, int mode,
+                      int max_rounds, float conv_eps, float* poses_out, int32_t* n_corr_out,
+                      int32_t* n_in_out, int32_t* rounds_out, int32_t* n_new_out,
+                      int64_t map_cap, float* map_xyz, float* map_desc) {
+  int64_t nmax = 0;
+  for (int64_t f = f0; f <= f0 + steps; ++f) nmax = frame_off[f + 1] - frame_off[f] > nmax ? frame_off[f + 1] - frame_off[f] : nmax;
+  const size_t nb = (size_t)(nmax > 0 ? nmax : 1);
+  int32_t* bi = (int32_t*)malloc(nb * 4);
+  int32_t* acc = (int32_t*)malloc(nb * 4);
+  int32_t* wacc = (int32_t*)malloc(nb * 4);
+  int32_t* ia = (int32_t*)malloc(nb * 4);
+  int32_t* ib = (int32_t*)malloc(nb * 4);
+  int32_t* pairs = (int32_t*)malloc(nb * 8);
+  float* bd = (float*)malloc(nb * 4);
+  float* sd = (float*)malloc(nb * 4);
+  int64_t map_n = 0;
+#define FR_N(f) (frame_off[(f) + 1] - frame_off[(f)])
+#define FR_UV(f) (uv + 2 * frame_off[(f)])
+#define FR_DESC(f) (desc + (int64_t)dim * frame_off[(f)])
+  /* bootstrap: match(first, second) -> triangulate(T0, T1) (exec/icp_test.cpp:44-58) */
+  {
+    const int64_t na = FR_N(f0), nbb = FR_N(f0 + 1);
+    or_match_points(FR_DESC(f0), na, FR_DESC(f0 + 1), nbb, dim, 0.2f, 0.8f, bi, bd, sd, acc);
+    int64_t q = 0;
+    for (int64_t i = 0; i < na; ++i)
+      if (acc[i]) { ia[q] = (int32_t)i; ib[q] = bi[i]; ++q; }
+    map_n = vo_append(K, T0, T1, FR_UV(f0), FR_UV(f0 + 1), FR_DESC(f0), dim, ia, ib, q, 0, map_cap,
+                      map_xyz, map_desc);
+    if (n_new_out) n_new_out[0] = (int32_t)q;
+  }
+  memcpy(poses_out, T0, 16 * sizeof(float)); /* poses = {T0} (:36 with the bootstrap frame) */
+  for (int t = 0; t < steps && map_n >= 0; ++t) {
+    const int64_t cf = f0 + t, nf = cf + 1;
+    const int64_t nc = FR_N(cf), nn = FR_N(nf);
+    /* corr = match(next, world) (:72-73); pairs (image idx, world idx) */
+    or_match_points(FR_DESC(nf), nn, map_desc, map_n, dim, 0.2f, 0.8f, bi, bd, sd, wacc);
+    int64_t m = 0;
+    for (int64_t i = 0; i < nn; ++i)
+      if (wacc[i]) { pairs[2 * m] = (int32_t)i; pairs[2 * m + 1] = bi[i]; ++m; }
+    /* PICP from the previous pose (:76-107) */
+    float T[16];
+    or_iso_inverse(poses_out + 16 * t, T);
+    or_stats_t st;
+    int conv = 0;
+    const int rounds = or_solve(T, K, rows, cols, map_xyz, FR_UV(nf), pairs, m, threshold, 1.0f, 0,
+                                0, mode, max_rounds, conv_eps, &st, &conv);
+    or_iso_inverse(T, poses_out + 16 * (t + 1)); /* :113 */
+    if (n_corr_out) n_corr_out[t] = (int32_t)m;
+    if (n_in_out) n_in_out[t] = st.n_in;
+    if (rounds_out) rounds_out[t] = rounds;
+    /* img matches curr -> next, add_new_world_points, triangulate (:117-130) */
+    or_match_points(FR_DESC(cf), nc, FR_DESC(nf), nn, dim, 0.2f, 0.8f, bi, bd, sd, acc);
+    int64_t q = 0;
+    for (int64_t i = 0; i < nc; ++i)
+      if (acc[i] && !wacc[bi[i]]) { ia[q] = (int32_t)i; ib[q] = bi[i]; ++q; }
+    map_n = vo_append(K, poses_out + 16 * t, poses_out + 16 * (t + 1), FR_UV(cf), FR_UV(nf), FR_DESC(cf),
+                      dim, ia, ib, q, map_n, map_cap, map_xyz, map_desc);
+    if (n_new_out) n_new_out[t + 1] = (int32_t)q;
+  }
+#undef FR_N
+#undef FR_UV
+#undef FR_DESC
+  free(bi); free(acc); free(wacc); free(ia); free(ib); free(pairs); free(bd); free(sd);
+  return map_n;
 }

@@ -115,6 +115,26 @@ int64_t or_match_points(const float* d1, int64_t n1, const float* d2, int64_t n2
                         float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
                         float* second_dist, int32_t* accepted);
 
+/* The VO loop of exec/icp_test.cpp:36-136 over one segment of a sequence:
+ * frames [f0, f0 + steps] of the packed observations (frame k = rows [frame_off[k],
+ * frame_off[k+1]) of uv (float2) and desc (float[dim])).
+ *   bootstrap (:40-58, with the pose pair given instead of computeEssentialAndRecoverPose):
+ *     pairs = match(frame f0, frame f0+1); map = triangulate(T0, T1, pairs) (descriptor of f0).
+ *   step t (:61-136): next = f0+t+1; corr = match(next, map); PICP from poses[t] (icp_test
+ *     loop: threshold, <= max_rounds, relative-chi conv_eps, keep_outliers false);
+ *     poses[t+1] = estimate; pairs = match(curr, next); add_new_world_points
+ *     (src/my_utilities.cpp:413-434): the pairs whose next point has no map match are
+ *     triangulated with (poses[t], poses[t+1]) and appended in pair order.
+ * Poses are camera-in-world (4x4 column-major).  Outputs: poses_out[(steps+1)*16] ([0] = T0),
+ * per step n_corr/n_in/rounds/n_new (n_new_out has steps+1 entries, [0] = bootstrap), the map
+ * (xyz[3*cap], desc[dim*cap]).  Returns the final map size, or -1 if map_cap is exceeded. */
+int64_t or_vo_segment(const float K[9], int rows, int cols, const int64_t* frame_off,
+                      const float* uv, const float* desc, int dim, int64_t f0, int steps,
+                      const float T0[16], const float T1[16], float threshold, int mode,
+                      int max_rounds, float conv_eps, float* poses_out, int32_t* n_corr_out,
+                      int32_t* n_in_out, int32_t* rounds_out, int32_t* n_new_out,
+                      int64_t map_cap, float* map_xyz, float* map_desc);
+
 /* Eigen::Isometry3f::inverse() (rigid inverse) */
 void or_iso_inverse(const float T[16], float Tinv[16]);
 

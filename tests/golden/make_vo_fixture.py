@@ -58,8 +58,13 @@ def main():
     # the reference's published run (output/errors.txt: frame, translational err, yaw err) -- a
     # loose end-to-end band only (UB-tainted, OpenCV-RANSAC bootstrap)
     errs = np.loadtxt(os.path.join(REF, "output", "errors.txt"), dtype=np.float64)
+    # the reference's final map (output/estimated_world_points.txt, exec/icp_test.cpp:199-211):
+    # for every id_real 0..999 the first map point carrying it -> the id column is the set of
+    # distinct landmarks the run triangulated (490, README:7).  Only the ids are kept: the
+    # coordinates depend on the RANSAC bootstrap and the umeyama scale.
+    wp = np.loadtxt(os.path.join(REF, "output", "estimated_world_points.txt"), dtype=np.float64)
     np.savez_compressed(
-        OUT, ref_errors=errs.astype(np.float32),
+        OUT, ref_errors=errs.astype(np.float32), ref_map_ids=wp[:, 0].astype(np.int32),
         world_id=np.array(wid, np.int32), world_xyz=np.array(wxyz, np.float32),
         world_desc=np.array(wdesc, np.float32),
         gt_pose=gt, odom_pose=odom,

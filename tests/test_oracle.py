@@ -284,3 +284,67 @@ def test_match_points_empty_sets(oracle):
     assert (got["best_idx"] == -1).all() and not got["accepted"].any()
     got = oracle.match_points(np.zeros((0, 10), np.float32), d)
     assert len(got["best_idx"]) == 0
+
+
+# ------------------------------------------------------------------ VO sequence (C1 / C5)
+def _data_sequence(vo):
+    from picp_amd.synth import MOUNT, planar
+    off, uv, desc = vo.packed()
+    Tc = [planar(*vo.gt_pose[k]) @ MOUNT for k in range(vo.n_frames)]
+    return off, uv, desc, Tc
+
+
+def test_kat_vo_loop_map_matches_reference_run(oracle, vo):
+    """The reference's own run of exec/icp_test.cpp wrote its final map to
+    output/estimated_world_points.txt: 490 distinct landmarks (README:7).  The restated loop
+    (match -> PICP -> match -> add_new_world_points -> triangulate) over data/ builds a map of
+    exactly those landmarks.  The composition depends on descriptor matching only, so it is
+    independent of the bootstrap pose (gt here, RANSAC in the reference)."""
+    off, uv, desc, Tc = _data_sequence(vo)
+    r = oracle.vo_segment(vo.K, vo.rows, vo.cols, off, uv, desc, 0, vo.n_frames - 1, Tc[0], Tc[1],
+                          mode=oracle.MODE_FAITHFUL)
+    ids = vo.map_ids(r["map_desc"])
+    assert len(ids) == 490 and (ids >= 0).all()
+    assert set(ids.tolist()) == set(vo.ref_map_ids.tolist())
+    # with the metric bootstrap the trajectory stays within a few cm of gt over 120 frames
+    e = [np.linalg.norm(r["poses"][k][:3, 3] - Tc[k][:3, 3]) for k in range(vo.n_frames)]
+    assert max(e) < 0.1
+
+
+def test_vo_synthetic_sequence_properties():
+    from picp_amd.vo_synth import VOSequence, segments
+    from picp_amd.synth import rigid_inverse
+    s = VOSequence(30, obs_per_frame=800, seed=5)
+    f = s.frame(7)
+    assert 600 < len(f["uv"]) < 1000
+    assert (f["id_meas"] == np.arange(len(f["uv"]))).all() and len(set(f["id_real"].tolist())) == len(f["uv"])
+    np.testing.assert_array_equal(s.frame(7)["uv"], f["uv"])  # deterministic per frame
+    F = s.frames(5, 9)
+    np.testing.assert_array_equal(F["uv"][F["frame_off"][2]:F["frame_off"][3]], f["uv"])
+    # every observation is the float32 projection of its landmark under the gt pose
+    lm = {}
+    for k in range(3, 40):
+        ids, xyz, _ = s.landmarks(k)
+        lm.update(zip(ids.tolist(), xyz))
+    P = np.array([lm[int(i)] for i in f["id_real"]])
+    T = rigid_inverse(s.T_cw(7))
+    pc = T[:3, :3] @ P.T + T[:3, 3:4]
+    uv = (s.K.astype(np.float64) @ pc)[:2] / pc[2]
+    np.testing.assert_allclose(uv.T, f["uv"], atol=1e-3)
+    assert (f["uv"] >= 0).all() and (f["uv"][:, 0] <= 639).all() and (f["uv"][:, 1] <= 479).all()
+    first, steps = segments(101, 25)
+    assert first.tolist() == [0, 25, 50, 75] and steps.tolist() == [25, 25, 25, 25]
+    first, steps = segments(90, 25)
+    assert first.tolist() == [0, 25, 50, 75] and steps.tolist() == [25, 25, 25, 14]
+
+
+def test_vo_oracle_tracks_synthetic_ground_truth(oracle):
+    from picp_amd.vo_synth import VOSequence
+    from picp_amd.synth import se3_log_norm, rigid_inverse
+    s = VOSequence(13, obs_per_frame=500, seed=3)
+    F = s.frames(0, 13)
+    r = oracle.vo_segment(s.K, 480, 640, F["frame_off"], F["uv"], F["desc"], 0, 12, F["T_cw"][0], F["T_cw"][1])
+    err = [se3_log_norm(rigid_inverse(r["poses"][k].astype(np.float64)), rigid_inverse(F["T_cw"][k].astype(np.float64)))
+           for k in range(13)]
+    assert max(err) < 5e-3
+    assert (r["n_corr"] > 300).all() and r["n_new"][0] > 300 and (r["n_new"][2:] > 0).all()
