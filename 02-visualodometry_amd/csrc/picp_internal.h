@@ -124,4 +124,5 @@ struct VoArgs {     // by value; every pointer is device memory
   MatchProblem* wprobs;      // next step's world-match problem of each segment
   float* poses;              // 16 per slot, camera-in-world, column-major
   VoStep* steps;
+  int2* pairs;               // append scratch: segment s at s * cap_c
 };

@@ -7,8 +7,11 @@
 // (src/my_utilities.h:44-46,100-103).  The distance is summed over the dims in order with FP
 // contraction off, so indices, distances and accept flags are bit-identical to the CPU oracle.
 //
-// One lane per query, the query's descriptor in registers; set 2 is streamed through LDS in
-// tiles shared by the 256 queries of a block.  Batched: blockIdx.y = problem (ragged sets).
+// Two queries per lane, their descriptors in registers as float2 pairs, so the subtract, square
+// and in-order accumulation of both run as packed fp32 (v_pk_add_f32 / v_pk_mul_f32: two exact
+// IEEE ops per lane per instruction -- FMA contraction is off, so the bits equal the oracle's);
+// set 2 is streamed through LDS in tiles shared by the 512 queries of a block, one broadcast LDS
+// read feeding both queries.  Batched: blockIdx.y = problem (ragged sets).
 #include <hip/hip_runtime.h>
 
 #include <float.h>
@@ -17,9 +20,26 @@
 #include "picp_internal.h"
 
 #define PICP_MATCH_BLOCK 256
+#define PICP_MATCH_QPL 2  // queries per lane: (query A, query B) packed in one float2
+#define PICP_MATCH_QPB (PICP_MATCH_BLOCK * PICP_MATCH_QPL)
 #define PICP_MATCH_TILE 256
 #define PICP_MATCH_MAXD 32
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// The reference's update (src/my_utilities.h:91-97), in index order,
+//   if (d < best) { second = best; best = d; bi = j; } else if (d < second) second = d;
+// branch-free for finite d >= 0 (best <= second always holds):
+//   second' = med3(best, d, second)   (d < best: best; best <= d < second: d; else second;
+//                                       d == best: best == d, as the reference's else-branch)
+//   best'   = d < best ? d : best
+//   bi'     = d < best ? j : bi       (strict: the first index of the minimum wins)
+__device__ inline void match_update(float d, int32_t j, float& best, float& second, int32_t& bi) {
+  const bool lt = d < best;
+  second = __builtin_amdgcn_fmed3f(best, d, second);
+  best = lt ? d : best;
+  bi = lt ? j : bi;
+}
 
 template <int D>  // D > 0: compile-time dim; D == 0: runtime dim <= PICP_MATCH_MAXD
 __global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(
@@ -29,51 +49,62 @@ __global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(
     float* __restrict__ second_dist, int32_t* __restrict__ accepted) {
   constexpr int DM = D > 0 ? D : PICP_MATCH_MAXD;
   const int dim = D > 0 ? D : dim_rt;
-  __shared__ float tile[PICP_MATCH_TILE * DM];
+  constexpr int TILE = DM <= 16 ? PICP_MATCH_TILE : PICP_MATCH_TILE / 2;
+  __shared__ f2 tile[TILE * DM];  // each value duplicated: one LDS read = both lanes of a pk op
   const MatchProblem P = probs[blockIdx.y];
-  const int64_t qi = (int64_t)blockIdx.x * PICP_MATCH_BLOCK + threadIdx.x;
-  if ((int64_t)blockIdx.x * PICP_MATCH_BLOCK >= P.nq) return;  // whole block past this problem
-  const bool active = qi < P.nq;
-  float q[DM];
+  const int64_t q0 = (int64_t)blockIdx.x * PICP_MATCH_QPB;
+  if (q0 >= P.nq) return;  // whole block past this problem
+  const int64_t qa = q0 + threadIdx.x, qb = qa + PICP_MATCH_BLOCK;
+  const bool va = qa < P.nq, vb = qb < P.nq;
+  f2 q[DM];
 #pragma unroll
-  for (int k = 0; k < DM; ++k) q[k] = (active && k < dim) ? q_desc[(P.q_off + qi) * dim + k] : 0.0f;
-  float best = FLT_MAX, second = FLT_MAX;  // src/my_utilities.h:78-79
-  int32_t bi = -1;
-  for (int64_t t0 = 0; t0 < P.nr; t0 += PICP_MATCH_TILE) {
-    const int nt = (int)((P.nr - t0) < PICP_MATCH_TILE ? (P.nr - t0) : PICP_MATCH_TILE);
+  for (int k = 0; k < DM; ++k) {
+    q[k].x = (va && k < dim) ? q_desc[(P.q_off + qa) * dim + k] : 0.0f;
+    q[k].y = (vb && k < dim) ? q_desc[(P.q_off + qb) * dim + k] : 0.0f;
+  }
+  float best_a = FLT_MAX, second_a = FLT_MAX, best_b = FLT_MAX, second_b = FLT_MAX;  // :78-79
+  int32_t bi_a = -1, bi_b = -1;
+  for (int64_t t0 = 0; t0 < P.nr; t0 += TILE) {
+    const int nt = (int)((P.nr - t0) < TILE ? (P.nr - t0) : TILE);
     __syncthreads();
-    for (int e = threadIdx.x; e < nt * dim; e += PICP_MATCH_BLOCK)
-      tile[e] = r_desc[(P.r_off + t0) * dim + e];
+    for (int e = threadIdx.x; e < nt * dim; e += PICP_MATCH_BLOCK) {
+      const float r = r_desc[(P.r_off + t0) * dim + e];
+      tile[e] = (f2){r, r};
+    }
     __syncthreads();
-    if (active) {
+    if (va) {
       for (int j = 0; j < nt; ++j) {
-        float d = 0.0f;
+        f2 d = {0.0f, 0.0f};
         {
 #pragma clang fp contract(off)
 #pragma unroll
           for (int k = 0; k < DM; ++k) {
-            if (k < dim) {
-              const float t = q[k] - tile[j * dim + k];
+            if (k < dim) {  // (a - r)^2 summed over the dims in order, per query
+              const f2 t = q[k] - tile[j * dim + k];
               d = d + t * t;
             }
           }
         }
-        if (d < best) {  // :91-97
-          second = best;
-          best = d;
-          bi = (int32_t)(t0 + j);
-        } else if (d < second) {
-          second = d;
-        }
+        const int32_t jj = (int32_t)(t0 + j);
+        match_update(d.x, jj, best_a, second_a, bi_a);
+        match_update(d.y, jj, best_b, second_b, bi_b);
       }
     }
   }
-  if (active) {
-    const int64_t o = P.q_off + qi;
-    best_idx[o] = bi;
-    best_dist[o] = best;
-    second_dist[o] = second;
-    accepted[o] = (bi != -1 && best < dist_thr && best / second < ratio_thr) ? 1 : 0;  // :100-103
+  // accepted iff best < DISTANCE_THRESHOLD and best/second < RATIO_THRESHOLD (:100-103)
+  if (va) {
+    const int64_t o = P.q_off + qa;
+    best_idx[o] = bi_a;
+    best_dist[o] = best_a;
+    second_dist[o] = second_a;
+    accepted[o] = (bi_a != -1 && best_a < dist_thr && best_a / second_a < ratio_thr) ? 1 : 0;
+  }
+  if (vb) {
+    const int64_t o = P.q_off + qb;
+    best_idx[o] = bi_b;
+    best_dist[o] = best_b;
+    second_dist[o] = second_b;
+    accepted[o] = (bi_b != -1 && best_b < dist_thr && best_b / second_b < ratio_thr) ? 1 : 0;
   }
 }
 
@@ -84,7 +115,7 @@ extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int6
                                         float* second_dist, int32_t* accepted) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((max_nq + PICP_MATCH_BLOCK - 1) / PICP_MATCH_BLOCK), (unsigned)n_problems);
+  const dim3 grid((unsigned)((max_nq + PICP_MATCH_QPB - 1) / PICP_MATCH_QPB), (unsigned)n_problems);
   if (dim == 10)
     hipLaunchKernelGGL(picp_match_kernel<10>, grid, dim3(PICP_MATCH_BLOCK), 0, stream, q_desc, r_desc,
                        probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted);

@@ -179,6 +179,8 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
   __syncthreads();
   const int64_t mbase = G.map_off + s_base;
   const int dim = a.dim;
+  int2* pairs = a.pairs + (int64_t)s * a.cap_c;
+  // pass 1: the selected (curr, next) pairs in pair order (add_new_world_points)
   int64_t cnt = 0;
   for (int64_t c0 = 0; c0 < nc; c0 += VO_BLOCK) {
     const int64_t i = c0 + threadIdx.x;
@@ -186,20 +188,24 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
     int j = 0;
     if (i < nc && a.pm_acc[oc + i]) {
       j = a.pm_bi[oc + i];
-      flag = boot || a.wm_acc[on + j] == 0;  // add_new_world_points: next point not in corr
+      flag = boot || a.wm_acc[on + j] == 0;  // next point not among the map correspondences
     }
     int tot;
     const int r = vo_block_rank(flag, s_cnt, &tot);
-    if (flag) {
-      const int64_t slot = mbase + cnt + r;
-      float o[3];
-      triangulate_dlt(sP, sP + 12, a.uv[oc + i], a.uv[on + j], o);
-      a.map_xyz[3 * slot + 0] = o[0];
-      a.map_xyz[3 * slot + 1] = o[1];
-      a.map_xyz[3 * slot + 2] = o[2];
-      for (int d = 0; d < dim; ++d) a.map_desc[slot * dim + d] = a.desc[(oc + i) * dim + d];
-    }
+    if (flag) pairs[cnt + r] = make_int2((int)i, j);
     cnt += tot;
+  }
+  __syncthreads();
+  // pass 2: every lane triangulates (src/cam.cpp:115-139) and appends (xyz, curr descriptor)
+  for (int64_t k = threadIdx.x; k < cnt; k += VO_BLOCK) {
+    const int2 pr = pairs[k];
+    const int64_t slot = mbase + k;
+    float o[3];
+    triangulate_dlt(sP, sP + 12, a.uv[oc + pr.x], a.uv[on + pr.y], o);
+    a.map_xyz[3 * slot + 0] = o[0];
+    a.map_xyz[3 * slot + 1] = o[1];
+    a.map_xyz[3 * slot + 2] = o[2];
+    for (int d = 0; d < dim; ++d) a.map_desc[slot * dim + d] = a.desc[(oc + pr.x) * dim + d];
   }
   if (threadIdx.x == 0) {
     const int64_t mn = s_base + cnt;

@@ -206,8 +206,11 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     if (is_curr[f] && frame_n(h, f) > 0)
       pprobs.push_back(MatchProblem{h->frame_off[f], frame_n(h, f), h->frame_off[f + 1], frame_n(h, f + 1)});
   int64_t cap_c = (std::max<int64_t>(h->max_obs, 1) + 3) / 4 * 4;
+  // register-resident items per lane of picp_block_kernel: the largest power of two whose
+  // 512 * npt slots the biggest frame fills (masked slots cost as much as live ones every
+  // round; the few items past npt * 512 take the kernel's streamed-remainder path)
   int npt = 1;
-  while (npt < 8 && (int64_t)npt * 512 < h->max_obs) npt *= 2;
+  while (npt < 8 && (int64_t)npt * 2 * 512 <= h->max_obs) npt *= 2;
 
   // one allocation for everything sized by the segments
   struct Part { size_t off, bytes; };
@@ -226,6 +229,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_pprobs = part(std::max<size_t>(pprobs.size(), 1) * sizeof(MatchProblem));
   const Part p_poses = part((size_t)n_slots * 16 * sizeof(float));
   const Part p_steps = part((size_t)n_slots * sizeof(VoStep));
+  const Part p_pairs = part((size_t)n_seg * cap_c * sizeof(int2));
   HIP_TRY(hipMalloc(&h->seg_mem, total));
   char* m = (char*)h->seg_mem;
   h->segs = segs;
@@ -288,6 +292,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   V.wprobs = (MatchProblem*)(m + p_wprobs.off);
   V.poses = (float*)(m + p_poses.off);
   V.steps = (VoStep*)(m + p_steps.off);
+  V.pairs = (int2*)(m + p_pairs.off);
   h->wprobs_d = V.wprobs;
   h->pprobs_d = (MatchProblem*)(m + p_pprobs.off);
   return PICP_OK;
@@ -355,8 +360,11 @@ extern "C" int picp_vo_run(picp_vo_t* h) {
 
 extern "C" int picp_vo_time(picp_vo_t* h, int reps, float* ms_per_run) {
   CHECK_ARG(h && ms_per_run && reps >= 1, "picp_vo_time: bad argument");
-  int rc = vo_launch(h);  // warm (and capture)
-  if (rc != PICP_OK) return rc;
+  int rc = PICP_OK;
+  if (h->use_graph && !h->exec) {  // capture outside the timed events
+    rc = vo_launch(h);
+    if (rc != PICP_OK) return rc;
+  }
   HIP_TRY(hipEventRecord(h->ev0, h->stream));
   for (int r = 0; r < reps; ++r) {
     rc = vo_launch(h);

@@ -37,6 +37,7 @@ WORKLOADS = {
     "c2": dict(n=100000, problems=1, outlier=0.0, desc="C2 single-frame PICP, 100k synthetic correspondences, 50 GN rounds"),
     "c3": dict(n=1000000, problems=1, outlier=0.3, desc="C3 single-frame PICP, 1M synthetic correspondences, 30% outliers + chi2 rejection, 50 GN rounds"),
     "c4": dict(n=10000, problems=128, outlier=0.0, desc="C4 batch of independent frames x 10k correspondences (128 per GPU), 50 GN rounds each"),
+    "c5": dict(frames=10000, obs=2000, desc="C5 full VO pipeline: 10k-frame synthetic sequence, per frame match -> PICP -> match -> triangulate on GPU, frame-parallel segments"),
 }
 
 
@@ -51,6 +52,9 @@ def main():
     ap.add_argument("--problems", type=int, default=0, help="override frames per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--frames", type=int, default=0, help="c5: sequence length (default 10000)")
+    ap.add_argument("--obs", type=int, default=0, help="c5: observations per frame (default 2000)")
+    ap.add_argument("--seg-len", type=int, default=40, help="c5: PICP steps per segment")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -67,6 +71,8 @@ def main():
     from picp_amd import synth
 
     wl = dict(WORKLOADS[args.workload])
+    if args.workload == "c5":
+        return bench_vo(args, wl, world, rank, local, dist, torch)
     n = args.n or wl["n"]
     nprob = args.problems or wl["problems"]
     R = args.rounds
@@ -181,6 +187,129 @@ def main():
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_vo(args, wl, world, rank, local, dist, torch):
+    """C5: the whole sequence is split into contiguous segments of --seg-len PICP steps (one-frame
+    overlap); ranks take contiguous ranges of segments (strong scaling: the
+    sequence is fixed).  One step = one replay of the captured run of this rank's segments
+    (pair matching of all its frames, bootstrap, then per frame: world match, gather, PICP block
+    kernel, triangulate/append).  value = frames estimated by all ranks / max-over-ranks time."""
+    import numpy as np
+    import picp_amd
+    from picp_amd import synth
+    from picp_amd.dist import shard_range
+    from picp_amd.vo_synth import VOSequence, segments
+    F = args.frames or wl["frames"]
+    obs = args.obs or wl["obs"]
+    L = args.seg_len
+    seq = VOSequence(F, obs_per_frame=obs, seed=42)
+    first, steps = segments(F, L)
+    s0, s1 = shard_range(len(first), world, rank)
+    fa, fb = int(first[s0]), int(first[s1 - 1] + steps[s1 - 1])
+    D = seq.frames(fa, fb + 1)
+    my_first, my_steps = first[s0:s1] - fa, steps[s0:s1]
+    # each segment's world frame is its first camera, as the reference's is frame 0's
+    # (exec/icp_test.cpp:36, bootstrap from Identity): float32 coordinates stay segment-sized
+    rel = [np.linalg.inv(D["T_cw"][f].astype(np.float64)) for f in my_first]
+    boot = np.stack([[np.eye(4), rel[k] @ D["T_cw"][f + 1]] for k, f in enumerate(my_first)]).astype(np.float32)
+    vo = picp_amd.VOSequence(D["frame_off"], D["uv"], D["desc"], device=local if world > 1 else 0, K=seq.K)
+    vo.set_segments(my_first, my_steps, boot, threshold=3000.0)
+
+    def sync_all():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    for _ in range(max(args.warmup, 1)):
+        vo.run()
+    sync_all()
+    if dist is not None:
+        dist.barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    ev_ms = vo.time(args.steps)
+    sync_all()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # correctness of what was timed: drift vs gt, PICP work done
+    P, Rr = vo.poses(), vo.step_records()
+    err, rounds, corr = 0.0, 0, 0
+    for k, f0 in enumerate(my_first):
+        for t in range(1, len(P[k])):
+            gt = rel[k] @ D["T_cw"][f0 + t].astype(np.float64)  # gt in the segment frame
+            err = max(err, synth.se3_log_norm(P[k][t].astype(np.float64), gt))
+        rounds += int(Rr[k]["rounds"][1:].sum())
+        corr += int((Rr[k]["rounds"][1:].astype(np.int64) * Rr[k]["n_corr"][1:]).sum())
+    stats = np.array([err, rounds, corr, int(my_steps.sum())], np.float64)
+    if dist is not None:
+        t = torch.tensor(stats, device="cuda")
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        e = t[:1].clone()
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        stats = t.cpu().numpy()
+        stats[0] = float(e.item())
+    frames_total = int(stats[3])
+    info = vo.info()
+    out = {
+        "metric": "VO frames/sec (%d-frame synthetic sequence, ~%d obs/frame, per-frame match + PICP + triangulate)" % (F, obs),
+        "value": round(frames_total * args.steps / elapsed, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic sequence (picp_amd/vo_synth.py, seed 42; observations resident in HBM)",
+        "config": {"workload": wl["desc"], "frames": F, "obs_per_frame": obs, "segment_steps": L,
+                   "segments": len(first), "segments_per_gpu": s1 - s0, "threshold": 3000.0,
+                   "picp_loop": "icp_test: <= 50 rounds, relative chi convergence 1e-5",
+                   "parallelism": "contiguous segment ranges, one process per GPU" if world > 1 else "single GPU",
+                   "block_npt": info["npt"]},
+        "picp_iterations_per_s": round(stats[1] * args.steps / elapsed, 1),
+        "picp_corr_rounds_per_s": round(stats[2] * args.steps / elapsed, 1),
+        "timed_region_event_ms": round(ev_ms * args.steps, 4),
+        "pose_err_vs_gt_se3_max": stats[0],
+        "pose_err_frame": "camera-in-world poses in each segment's frame (its first camera)",
+    }
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_vo(seq, L, budget_s):
+    """Oracle VO loop (faithful float32, 1 thread) over whole segments of the same sequence
+    until the budget is used: frames/s."""
+    import numpy as np
+    import oracle as O
+    D = seq.frames(0, min(seq.n_frames, 4 * L + 1))
+    frames, t0, f0 = 0, time.perf_counter(), 0
+    while True:
+        st = min(L, len(D["frame_off"]) - 2 - f0)
+        if st < 1:
+            f0 = 0
+            continue
+        T1 = (np.linalg.inv(D["T_cw"][f0].astype(np.float64)) @ D["T_cw"][f0 + 1]).astype(np.float32)
+        O.vo_segment(seq.K, 480, 640, D["frame_off"], D["uv"], D["desc"], f0, st, np.eye(4, dtype=np.float32),
+                     T1, mode=O.MODE_FAITHFUL)
+        frames += st
+        f0 += L
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "%d frames in %d-step segments of the same sequence (oracle VO loop, faithful "
+                      "float32, gcc -O2, 1 thread) in %.1f s" % (frames, L, el)}
 
 
 def cpu_baseline(xyz, uv, T_init, R, thr, budget_s):
