@@ -15,7 +15,7 @@ using namespace picp;
 
 #define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs
 
-template <int NPT>
+template <int NPT, int PH>
 __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
@@ -77,6 +77,7 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
   C.maxx = A.maxx;
   C.maxy = A.maxy;
   const float thr = A.threshold;
+  const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
 
   for (int round = 1; !s_done; ++round) {
@@ -85,32 +86,24 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
     T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
-    Acc a;
+    Acc2 a;
+    acc2_zero(a);
 #pragma unroll
-    for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
-    a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k)
-      accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], tid + k * PICP_BBLOCK < n, a);
+    for (int k = 0; k < NPT; k += 2) {  // pairs (k, k+1); NPT == 1: slot B repeats item 0, masked
+      const int k1 = (k + 1 < NPT) ? k + 1 : k;
+      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]},
+                      (f2){zs[k], zs[k1]}, (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]},
+                      tid + k * PICP_BBLOCK < n, k + 1 < NPT && tid + (k + 1) * PICP_BBLOCK < n, a);
+    }
     for (int i = NPT * PICP_BBLOCK + tid; i < n; i += 2 * PICP_BBLOCK) {  // streamed remainder
       const int i2 = min(i + PICP_BBLOCK, n - 1);
       const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
       const float x1 = X[base + i2], y1 = Y[base + i2], z1 = Z[base + i2], u1 = U[base + i2], v1 = V[base + i2];
-      accumulate_one(T, C, thr, keep, x0, y0, z0, u0, v0, true, a);
-      accumulate_one(T, C, thr, keep, x1, y1, z1, u1, v1, i + PICP_BBLOCK < n, a);
+      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
+                      (f2){v0, v1}, true, i + PICP_BBLOCK < n, a);
     }
     float v[PICP_NPART];
-#pragma unroll
-    for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
-    v[PICP_P_CHI_IN] = a.chi_in;
-    v[PICP_P_CHI_OUT] = a.chi_out;
-    v[PICP_P_N_IN] = a.n_in;
-    v[PICP_P_N_PROJ] = a.n_proj;
-    v[31] = 0.0f;
+    acc2_fold(a, v);
     const float wsum = wave_reduce32(v, lane);
     if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
     __syncthreads();
@@ -147,9 +140,14 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
                                         const PicpProblem* probs, const PicpState* st_in,
                                         PicpState* st_out) {
   if (grid <= 0 || !args) return hipErrorInvalidValue;
-#define PICP_LAUNCH_B(N)                                                                           \
-  hipLaunchKernelGGL(picp_block_kernel<N>, dim3(grid), dim3(PICP_BBLOCK), 0, stream, X, Y, Z, U, V, \
-                     *args, probs, st_in, st_out)
+  const bool ph = picp_use_pinhole(args->K);
+#define PICP_LAUNCH_B(N)                                                                                \
+  if (ph)                                                                                               \
+    hipLaunchKernelGGL((picp_block_kernel<N, 1>), dim3(grid), dim3(PICP_BBLOCK), 0, stream, X, Y, Z, U, \
+                       V, *args, probs, st_in, st_out);                                                \
+  else                                                                                                  \
+    hipLaunchKernelGGL((picp_block_kernel<N, 0>), dim3(grid), dim3(PICP_BBLOCK), 0, stream, X, Y, Z, U, \
+                       V, *args, probs, st_in, st_out)
   switch (npt) {
     case 1: PICP_LAUNCH_B(1); break;
     case 2: PICP_LAUNCH_B(2); break;

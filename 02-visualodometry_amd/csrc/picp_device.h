@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <float.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include "picp_internal.h"
@@ -28,6 +29,39 @@ struct Acc {
   float b[6];
   float chi_in, chi_out, n_in, n_proj;
 };
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Two accumulation slots per lane: correspondences are processed in PAIRS, item A in .x and
+// item B in .y of every value, so each arithmetic step of both is ONE packed fp32 instruction
+// (v_pk_mul/add/fma_f32: two exact IEEE operations, no operand shuffles); the slots are folded
+// once per thread at the end.
+struct Acc2 {
+  f2 h[21];
+  f2 b[6];
+  f2 chi_in, chi_out, n_in, n_proj;
+};
+
+__device__ __forceinline__ void acc2_zero(Acc2& a) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) a.h[i] = (f2){0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a.b[i] = (f2){0.0f, 0.0f};
+  a.chi_in = a.chi_out = a.n_in = a.n_proj = (f2){0.0f, 0.0f};
+}
+
+// fold the two slots into the 32-term partial layout (picp_internal.h PICP_P_*)
+__device__ __forceinline__ void acc2_fold(const Acc2& a, float v[PICP_NPART]) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i].x + a.h[i].y;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i].x + a.b[i].y;
+  v[PICP_P_CHI_IN] = a.chi_in.x + a.chi_in.y;
+  v[PICP_P_CHI_OUT] = a.chi_out.x + a.chi_out.y;
+  v[PICP_P_N_IN] = a.n_in.x + a.n_in.y;
+  v[PICP_P_N_PROJ] = a.n_proj.x + a.n_proj.y;
+  v[31] = 0.0f;
+}
 
 // ---------------------------------------------------------------------------------------
 // Per-correspondence math.  The block that decides projectability and the chi2 gate is
@@ -118,6 +152,314 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
     a.b[i] = fmaf(W0[i], e0, fmaf(W1[i], e1, a.b[i]));
   }
 }
+
+// Pinhole camera K = [fx 0 cx; 0 fy cy; 0 0 1] (the reference's K, src/cam.cpp:11-16; the
+// runtime selects this path only when K has exactly that structure).  Every term the general
+// form multiplies by one of K's zeros is an exact +-0 and K(2,2) = 1 makes ph2 == pc2, so with
+// those terms dropped the projection, bounds test, error and chi -- the gate -- AND the
+// Jacobian, evaluated in the oracle's operation order with contraction off
+// (oracle/picp_oracle.c or_error_and_jacobian: (Jp*K)*[I | skew(-pc)]), are bit-identical to
+// the reference arithmetic for finite inputs (a sign of zero can differ only where pc2 == 0,
+// which is rejected):
+//   a00 = fx/z, a02 = cx/z - ph0/z^2, a11 = fy/z, a12 = cy/z - ph1/z^2
+//   J0 = [a00, 0, a02, a02 pc1, a00 pc2 - a02 pc0, -a00 pc1]
+//   J1 = [0, a11, a12, a12 pc1 - a11 pc2, -a12 pc0, a11 pc0]
+// The structural zeros drop 12 of the 54 multiply-adds of H and b, and lambda = sqrt(thr/chi)
+// comes from v_rsq (it only weighs kept outliers, within the H/b tolerance): ~1/3 fewer VALU
+// instructions per correspondence than the general path.
+__device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, float thr,
+                                                   float inv_thr, bool keep, float x, float y,
+                                                   float z, float u, float v, bool in_range,
+                                                   Acc& a) {
+  float pc0, pc1, pc2, ph0, ph1, iz, e0, e1, chi;
+  bool valid;
+  {
+#pragma clang fp contract(off)
+    pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;  // src/camera.h:26
+    pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
+    pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
+    ph0 = C.k00 * pc0 + C.k02 * pc2;  // src/camera.h:29 without the zero terms
+    ph1 = C.k11 * pc1 + C.k12 * pc2;
+    iz = 1.0f / pc2;                  // ph2 == pc2 exactly
+    const float ix = ph0 * iz;
+    const float iy = ph1 * iz;
+    valid = in_range && !(pc2 <= 0.0f) &&
+            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    e0 = ix - u;
+    e1 = iy - v;
+    chi = e0 * e0 + e1 * e1;
+  }
+  const bool outlier = chi > thr;
+  const bool inl = valid && !outlier;
+  const bool use = inl || (valid && keep);
+  const float lambda = __builtin_amdgcn_rsqf(chi * inv_thr);
+  const float w = use ? (inl ? 1.0f : lambda) : 0.0f;
+  a.chi_in += inl ? chi : 0.0f;
+  a.chi_out += (valid && outlier) ? chi : 0.0f;
+  a.n_in += inl ? 1.0f : 0.0f;
+  a.n_proj += valid ? 1.0f : 0.0f;
+  // a skipped point gets weight 0 and finite inputs, so it can never inject inf/NaN
+  iz = use ? iz : 0.0f;
+  pc0 = use ? pc0 : 0.0f;
+  pc1 = use ? pc1 : 0.0f;
+  pc2 = use ? pc2 : 0.0f;
+  ph0 = use ? ph0 : 0.0f;
+  ph1 = use ? ph1 : 0.0f;
+  e0 = use ? e0 : 0.0f;
+  e1 = use ? e1 : 0.0f;
+  float J0[6], J1[6];
+  {
+#pragma clang fp contract(off)
+    const float iz2 = iz * iz;  // src/picp_solver.cpp:45-50
+    const float jp0 = -(ph0 * iz2), jp1 = -(ph1 * iz2);
+    const float a00 = iz * C.k00, a02 = iz * C.k02 + jp0;
+    const float a11 = iz * C.k11, a12 = iz * C.k12 + jp1;
+    J0[0] = a00; J0[1] = 0.0f; J0[2] = a02;
+    J0[3] = a02 * pc1;
+    J0[4] = a00 * pc2 - a02 * pc0;
+    J0[5] = -(a00 * pc1);
+    J1[0] = 0.0f; J1[1] = a11; J1[2] = a12;
+    J1[3] = -(a11 * pc2) + a12 * pc1;
+    J1[4] = -(a12 * pc0);
+    J1[5] = a11 * pc0;
+  }
+  float W0[6], W1[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    W0[i] = w * J0[i];
+    W1[i] = w * J1[i];
+  }
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      float h = a.h[k];
+      if (i != 0 && j != 0) h = fmaf(W1[i], J1[j], h);  // J1[0] == 0
+      if (i != 1 && j != 1) h = fmaf(W0[i], J0[j], h);  // J0[1] == 0
+      a.h[k] = h;
+      ++k;
+    }
+    float bb = a.b[i];
+    if (i != 0) bb = fmaf(W1[i], e1, bb);
+    if (i != 1) bb = fmaf(W0[i], e0, bb);
+    a.b[i] = bb;
+  }
+}
+
+// The general-K per-item math of accumulate_one up to the weighted Jacobian (for the packed
+// pair accumulation): outputs are zeroed for an unused item, w is its kernel weight.
+struct Item {
+  float J0[6], J1[6], e0, e1, w, chi;
+  bool inl, valid;
+};
+
+__device__ __forceinline__ void item_general(const Pose& T, const Cam& C, float thr, bool keep,
+                                             float x, float y, float z, float u, float v,
+                                             bool in_range, Item& o) {
+  float pc0, pc1, pc2, ph0, ph1, ph2, iz, e0, e1, chi;
+  bool valid;
+  {
+#pragma clang fp contract(off)
+    pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;
+    pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
+    pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
+    ph0 = (C.k00 * pc0 + C.k01 * pc1) + C.k02 * pc2;
+    ph1 = (C.k10 * pc0 + C.k11 * pc1) + C.k12 * pc2;
+    ph2 = (C.k20 * pc0 + C.k21 * pc1) + C.k22 * pc2;
+    iz = 1.0f / ph2;
+    const float ix = ph0 * iz;
+    const float iy = ph1 * iz;
+    valid = in_range && !(pc2 <= 0.0f) &&
+            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    e0 = ix - u;
+    e1 = iy - v;
+    chi = e0 * e0 + e1 * e1;
+  }
+  const bool outlier = chi > thr;
+  const bool inl = valid && !outlier;
+  const bool use = inl || (valid && keep);
+  const float lambda = outlier ? sqrtf(thr / chi) : 1.0f;
+  o.w = use ? (inl ? 1.0f : lambda) : 0.0f;
+  o.chi = chi;
+  o.inl = inl;
+  o.valid = valid;
+  iz = use ? iz : 0.0f;
+  pc0 = use ? pc0 : 0.0f;
+  pc1 = use ? pc1 : 0.0f;
+  pc2 = use ? pc2 : 0.0f;
+  ph0 = use ? ph0 : 0.0f;
+  ph1 = use ? ph1 : 0.0f;
+  o.e0 = use ? e0 : 0.0f;
+  o.e1 = use ? e1 : 0.0f;
+  const float iz2 = iz * iz;
+  const float jp02 = -ph0 * iz2, jp12 = -ph1 * iz2;
+  const float a00 = iz * C.k00 + jp02 * C.k20;
+  const float a01 = iz * C.k01 + jp02 * C.k21;
+  const float a02 = iz * C.k02 + jp02 * C.k22;
+  const float a10 = iz * C.k10 + jp12 * C.k20;
+  const float a11 = iz * C.k11 + jp12 * C.k21;
+  const float a12 = iz * C.k12 + jp12 * C.k22;
+  o.J0[0] = a00; o.J0[1] = a01; o.J0[2] = a02;
+  o.J0[3] = a02 * pc1 - a01 * pc2;
+  o.J0[4] = a00 * pc2 - a02 * pc0;
+  o.J0[5] = a01 * pc0 - a00 * pc1;
+  o.J1[0] = a10; o.J1[1] = a11; o.J1[2] = a12;
+  o.J1[3] = a12 * pc1 - a11 * pc2;
+  o.J1[4] = a10 * pc2 - a12 * pc0;
+  o.J1[5] = a11 * pc0 - a10 * pc1;
+}
+
+// H += w (J0^T J0 + J1^T J1), b += w (J0^T e0 + J1^T e1) for both slots; SPARSE skips the
+// pinhole Jacobian's structural zeros J0[1] = J1[0] = 0
+template <bool SPARSE>
+__device__ __forceinline__ void acc2_normal(const f2 J0[6], const f2 J1[6], f2 e0, f2 e1, f2 w,
+                                            Acc2& a) {
+  f2 W0[6], W1[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    W0[i] = w * J0[i];
+    W1[i] = w * J1[i];
+  }
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      f2 h = a.h[k];
+      if (!SPARSE || (i != 0 && j != 0)) h = __builtin_elementwise_fma(W1[i], J1[j], h);
+      if (!SPARSE || (i != 1 && j != 1)) h = __builtin_elementwise_fma(W0[i], J0[j], h);
+      a.h[k] = h;
+      ++k;
+    }
+    f2 bb = a.b[i];
+    if (!SPARSE || i != 0) bb = __builtin_elementwise_fma(W1[i], e1, bb);
+    if (!SPARSE || i != 1) bb = __builtin_elementwise_fma(W0[i], e0, bb);
+    a.b[i] = bb;
+  }
+}
+
+__device__ __forceinline__ void acc2_stats(f2 chi, bool inlA, bool inlB, bool validA, bool validB,
+                                           Acc2& a) {
+  a.chi_in += (f2){inlA ? chi.x : 0.0f, inlB ? chi.y : 0.0f};
+  a.chi_out += (f2){(validA && !inlA) ? chi.x : 0.0f, (validB && !inlB) ? chi.y : 0.0f};
+  a.n_in += (f2){inlA ? 1.0f : 0.0f, inlB ? 1.0f : 0.0f};
+  a.n_proj += (f2){validA ? 1.0f : 0.0f, validB ? 1.0f : 0.0f};
+}
+
+// A pair of correspondences, pinhole K: accumulate_pinhole's exact arithmetic with every
+// elementwise step packed (A in .x, B in .y).  Only the correctly rounded reciprocal, the
+// compares and the selects stay per item.  Contraction is off exactly where the oracle has it
+// off (gate and Jacobian), so both items are bit-identical to the scalar path.
+__device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C, float thr,
+                                                    float inv_thr, bool keep, f2 x, f2 y, f2 z,
+                                                    f2 u, f2 v, bool inA, bool inB, Acc2& a) {
+  f2 pc0, pc1, pc2, ph0, ph1, iz, e0, e1, chi;
+  bool validA, validB;
+  {
+#pragma clang fp contract(off)
+    pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;  // src/camera.h:26
+    pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
+    pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
+    ph0 = C.k00 * pc0 + C.k02 * pc2;  // src/camera.h:29 without the zero terms
+    ph1 = C.k11 * pc1 + C.k12 * pc2;
+    iz.x = 1.0f / pc2.x;              // ph2 == pc2 exactly; correctly rounded per item
+    iz.y = 1.0f / pc2.y;
+    const f2 ix = ph0 * iz;
+    const f2 iy = ph1 * iz;
+    validA = inA && !(pc2.x <= 0.0f) &&
+             !(ix.x < 0.0f || ix.x > C.maxx || iy.x < 0.0f || iy.x > C.maxy);
+    validB = inB && !(pc2.y <= 0.0f) &&
+             !(ix.y < 0.0f || ix.y > C.maxx || iy.y < 0.0f || iy.y > C.maxy);
+    e0 = ix - u;
+    e1 = iy - v;
+    chi = e0 * e0 + e1 * e1;
+  }
+  const bool outA = chi.x > thr, outB = chi.y > thr;
+  const bool inlA = validA && !outA, inlB = validB && !outB;
+  const bool useA = inlA || (validA && keep), useB = inlB || (validB && keep);
+  const f2 q = chi * inv_thr;
+  const f2 w = {useA ? (inlA ? 1.0f : __builtin_amdgcn_rsqf(q.x)) : 0.0f,
+                useB ? (inlB ? 1.0f : __builtin_amdgcn_rsqf(q.y)) : 0.0f};
+  acc2_stats(chi, inlA, inlB, validA, validB, a);
+  // a skipped item gets weight 0 and finite inputs, so it can never inject inf/NaN
+#define PICP_Z2(val) val = (f2){useA ? val.x : 0.0f, useB ? val.y : 0.0f}
+  PICP_Z2(iz); PICP_Z2(pc0); PICP_Z2(pc1); PICP_Z2(pc2); PICP_Z2(ph0); PICP_Z2(ph1); PICP_Z2(e0); PICP_Z2(e1);
+#undef PICP_Z2
+  f2 J0[6], J1[6];
+  {
+#pragma clang fp contract(off)
+    const f2 iz2 = iz * iz;  // src/picp_solver.cpp:45-52, the oracle's operation order
+    const f2 jp0 = -(ph0 * iz2), jp1 = -(ph1 * iz2);
+    const f2 a00 = iz * C.k00, a02 = iz * C.k02 + jp0;
+    const f2 a11 = iz * C.k11, a12 = iz * C.k12 + jp1;
+    const f2 zero = {0.0f, 0.0f};
+    J0[0] = a00; J0[1] = zero; J0[2] = a02;
+    J0[3] = a02 * pc1;
+    J0[4] = a00 * pc2 - a02 * pc0;
+    J0[5] = -(a00 * pc1);
+    J1[0] = zero; J1[1] = a11; J1[2] = a12;
+    J1[3] = -(a11 * pc2) + a12 * pc1;
+    J1[4] = -(a12 * pc0);
+    J1[5] = a11 * pc0;
+  }
+  acc2_normal<true>(J0, J1, e0, e1, w, a);
+}
+
+// A pair of correspondences, general K: per-item math (item_general), packed accumulation.
+__device__ __forceinline__ void accumulate_general2(const Pose& T, const Cam& C, float thr, bool keep,
+                                                    f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
+                                                    bool inB, Acc2& a) {
+  Item A, B;
+  item_general(T, C, thr, keep, x.x, y.x, z.x, u.x, v.x, inA, A);
+  item_general(T, C, thr, keep, x.y, y.y, z.y, u.y, v.y, inB, B);
+  acc2_stats((f2){A.chi, B.chi}, A.inl, B.inl, A.valid, B.valid, a);
+  f2 J0[6], J1[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    J0[i] = (f2){A.J0[i], B.J0[i]};
+    J1[i] = (f2){A.J1[i], B.J1[i]};
+  }
+  acc2_normal<false>(J0, J1, (f2){A.e0, B.e0}, (f2){A.e1, B.e1}, (f2){A.w, B.w}, a);
+}
+
+template <int PH>
+__device__ __forceinline__ void accumulate2(const Pose& T, const Cam& C, float thr, float inv_thr,
+                                            bool keep, f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
+                                            bool inB, Acc2& a) {
+  if constexpr (PH)
+    accumulate_pinhole2(T, C, thr, inv_thr, keep, x, y, z, u, v, inA, inB, a);
+  else
+    accumulate_general2(T, C, thr, keep, x, y, z, u, v, inA, inB, a);
+}
+
+// one correspondence with the camera path chosen at compile time (PH = pinhole K)
+template <int PH>
+__device__ __forceinline__ void accumulate(const Pose& T, const Cam& C, float thr, float inv_thr,
+                                           bool keep, float x, float y, float z, float u,
+                                           float v, bool in_range, Acc& a) {
+  if constexpr (PH)
+    accumulate_pinhole(T, C, thr, inv_thr, keep, x, y, z, u, v, in_range, a);
+  else
+    accumulate_one(T, C, thr, keep, x, y, z, u, v, in_range, a);
+}
+
+__host__ __device__ inline bool is_pinhole(const float K[9]) {  // column-major K
+  return K[1] == 0.0f && K[2] == 0.0f && K[3] == 0.0f && K[5] == 0.0f && K[8] == 1.0f;
+}
+
+}  // namespace picp
+
+// launch-time camera path: pinhole unless K is general or PICP_FORCE_GENERAL_K=1 (A/B checks)
+inline bool picp_use_pinhole(const float K[9]) {
+  static const bool force_general = [] {
+    const char* e = getenv("PICP_FORCE_GENERAL_K");
+    return e && atoi(e) != 0;
+  }();
+  return !force_general && picp::is_pinhole(K);
+}
+
+namespace picp {
 
 // Cross-lane moves without the LDS crossbar.  gfx950 v_permlane32_swap / v_permlane16_swap
 // exchange half-waves / odd-even 16-lane rows between two registers; DPP reads a partner

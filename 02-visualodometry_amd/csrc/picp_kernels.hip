@@ -1,13 +1,14 @@
 // picp_kernels.hip -- hand-written gfx950 (MI355X / CDNA4) kernels of the PICP hot path.
 //
 //   picp_round_kernel   one Gauss-Newton round of a batch of PICP problems:
-//                       prologue  = finish the previous round (deterministic double reduce of
-//                                   the block partials, damped 6x6 LDL^T solve, v2tEuler
-//                                   left-update, icp_test convergence test);
 //                       body      = linearize: one lane per correspondence, float4 SoA loads,
 //                                   projection + 2x6 Jacobian + chi2 gate in registers,
 //                                   halving-butterfly wave64 reduction of the 31 normal-equation
-//                                   terms, LDS cross-wave sum, one 128 B partial per block.
+//                                   terms, LDS cross-wave sum, one 128 B partial per block
+//                                   published write-through + an arrival ticket;
+//                       last arriver = finish the round (deterministic double reduce of the
+//                                   block partials, damped 6x6 LDL^T solve, v2tEuler
+//                                   left-update, icp_test convergence test).
 //   picp_gather_kernel  IntPairVector gather (image idx, world idx) -> SoA planes.
 //   picp_triangulate_kernel  batched two-view DLT (cv::triangulatePoints replacement).
 //
@@ -29,7 +30,7 @@
 __device__ unsigned long long picp_stamps[2][PICP_STAMP_BLOCKS][8];
 #define STAMP(k)                                                                         \
   do {                                                                                   \
-    if (threadIdx.x == 0 && !finalize && (j == 10 || j == 11) && blockIdx.x < PICP_STAMP_BLOCKS) \
+    if (threadIdx.x == 0 && (j == 10 || j == 11) && blockIdx.x < PICP_STAMP_BLOCKS) \
       picp_stamps[j - 10][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();              \
   } while (0)
 #else
@@ -43,45 +44,42 @@ __device__ unsigned long long picp_stamps[2][PICP_STAMP_BLOCKS][8];
 
 using namespace picp;
 
-// Deterministic sum of a problem's block partials (nblk x 32 floats) in double.  Lane t reads
-// float4 quad (t & 7) of blocks (t >> 3) + 32*u: all PICP_RED_UNROLL loads of a sweep are
-// issued before the first add (out-of-range slots re-read the last block and are masked, so
-// no load sits behind a branch), i.e. one memory latency per 32*PICP_RED_UNROLL blocks.  Then a
-// fixed-order LDS combine.  Result in s_tot[0..31]; all threads call; ends with a barrier.
-#define PICP_RED_UNROLL 16
-__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int blk0, int nblk,
-                                                double (*s_red)[PICP_NPART + 1], double* s_tot,
-                                                int32_t* st_slot, int32_t st_word) {
+// Last-arriver reduction of one problem's published partials (the guide's in-launch split-K
+// combine, cdna_hip_programming.md §6 Guideline 16): every partial word was stored write-through
+// (sc1) and drained before its block took the ticket, so EVERY load here is an sc1 load
+// (relaxed agent-scope atomic), which no CU's L1 can serve stale, on any XCD.  Thread t sums
+// column (t & 15) -- two floats of the 32 -- over rows (t >> 4) + 16k in double, then a
+// fixed-order LDS combine: deterministic for a given block partition.  Result in s_tot[0..31].
+#define PICP_RED_UNROLL 32  // 16 x 32 = 512 partials per sweep: one load latency for <= 512 blocks
+__device__ __forceinline__ void reduce_published(const unsigned long long* __restrict__ part, int blk0,
+                                                 int nblk, double (*s_red)[PICP_NPART + 1],
+                                                 double* s_tot) {
   const int tid = threadIdx.x;
-  const int q = tid & 7, r = tid >> 3;  // PICP_BLOCK/8 = 32 block slots per sweep
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  const float4* p4 = reinterpret_cast<const float4*>(part + (size_t)blk0 * PICP_NPART) + q;
-  for (int base = 0; base < nblk; base += 32 * PICP_RED_UNROLL) {
-    float4 v[PICP_RED_UNROLL];
+  const int c = tid & 15, r = tid >> 4;  // 16 row groups x 16 u64 columns
+  double lo = 0.0, hi = 0.0;
+  const unsigned long long* col = part + (size_t)blk0 * (PICP_NPART / 2) + c;
+  for (int base = 0; base < nblk; base += 16 * PICP_RED_UNROLL) {
+    unsigned long long w[PICP_RED_UNROLL];
 #pragma unroll
     for (int u = 0; u < PICP_RED_UNROLL; ++u) {
-      const int bb = min(base + u * 32 + r, nblk - 1);
-      v[u] = p4[(size_t)bb * (PICP_NPART / 4)];
+      const int bb = min(base + u * 16 + r, nblk - 1);
+      w[u] = __hip_atomic_load(col + (size_t)bb * (PICP_NPART / 2), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int u = 0; u < PICP_RED_UNROLL; ++u) {
-      const bool ok = base + u * 32 + r < nblk;
-      a0 += ok ? (double)v[u].x : 0.0;
-      a1 += ok ? (double)v[u].y : 0.0;
-      a2 += ok ? (double)v[u].z : 0.0;
-      a3 += ok ? (double)v[u].w : 0.0;
+      const bool ok = base + u * 16 + r < nblk;
+      lo += ok ? (double)__uint_as_float((unsigned)(w[u] & 0xffffffffull)) : 0.0;
+      hi += ok ? (double)__uint_as_float((unsigned)(w[u] >> 32)) : 0.0;
     }
   }
-  s_red[r][4 * q + 0] = a0;
-  s_red[r][4 * q + 1] = a1;
-  s_red[r][4 * q + 2] = a2;
-  s_red[r][4 * q + 3] = a3;
-  if (st_slot) *st_slot = st_word;
+  s_red[r][2 * c] = lo;
+  s_red[r][2 * c + 1] = hi;
   __syncthreads();
   if (tid < PICP_NPART) {
     double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
 #pragma unroll
-    for (int k = 0; k < 32; k += 4) {
+    for (int k = 0; k < 16; k += 4) {
       t0 += s_red[k + 0][tid];
       t1 += s_red[k + 1][tid];
       t2 += s_red[k + 2][tid];
@@ -92,32 +90,35 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
   __syncthreads();
 }
 
-// Launch j (0 <= j <= R) of the fused R-round solve.  Launch j finishes round j-1 (j>0) and,
-// unless the problem is done, linearizes round j.  With finalize=1 only the finishing part
-// runs, one block per problem.  State and partials ping-pong between launches, so no
-// inter-workgroup synchronisation is ever needed inside a launch: the kernel boundary is the
-// only hand-off.  VEC = correspondences per lane per chunk (4: float4 loads, for large
-// batches; 1: one per lane, to spread a single frame over every SIMD).
-template <int VEC>
+// Launch j (0 <= j < R) of the fused R-round solve: every block of a live problem linearizes
+// round j+1 over its slice at the pose in st_in, reduces it (wave64 permlane/DPP + LDS), and
+// publishes its 32-float partial write-through; the LAST block of the problem to take the
+// arrival ticket reduces all of them (deterministic order), runs finish_round (damping, LDL^T,
+// Rx*Ry*Rz update, icp_test convergence) and writes st_out.  One state read per block per
+// round instead of a sweep of every partial: the launch boundary is the only other hand-off.
+// Finished problems propagate their state through the ping-pong.  VEC = correspondences per
+// lane per chunk (4: float4 loads, for large batches; 1: one per lane, to spread a single frame
+// over every SIMD).  tickets[p] are zeroed by a memset node before launch 0 and re-zeroed by
+// each last arriver.
+template <int VEC, int PH>
 __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const int4* __restrict__ blkinfo,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
-    const float* __restrict__ part_in, float* __restrict__ part_out, int j, int finalize) {
-  __shared__ double s_red[32][PICP_NPART + 1];
+    unsigned long long* __restrict__ part, unsigned int* __restrict__ tickets, int j) {
+  __shared__ double s_red[16][PICP_NPART + 1];
   __shared__ double s_tot[PICP_NPART];
   __shared__ float s_wave[PICP_BLOCK / 64][PICP_NPART];
-  __shared__ float s_pose[12];
   __shared__ int32_t s_state[32];
-  __shared__ int s_go;
+  __shared__ int s_last;
 
   const int tid = threadIdx.x;
   STAMP(0);
   int p, first = 0, count = 0, blk0, nblk;
   int64_t base;
   if (A.uniform) {
-    p = finalize ? (int)blockIdx.x : (int)blockIdx.x / A.nblk_u;
+    p = (int)blockIdx.x / A.nblk_u;
     const int kb = (int)blockIdx.x - p * A.nblk_u;
     first = kb * A.ipb;
     count = max(0, min(A.ipb, A.n_u - first));
@@ -125,100 +126,87 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
     nblk = A.nblk_u;
     base = (int64_t)p * A.stride_u + first;
   } else {
-    if (finalize) {
-      p = blockIdx.x;
-    } else {
-      const int4 bi = blkinfo[blockIdx.x];
-      p = bi.x;
-      first = bi.y;
-      count = bi.z;
-    }
+    const int4 bi = blkinfo[blockIdx.x];
+    p = bi.x;
+    first = bi.y;
+    count = bi.z;
     const PicpProblem P = probs[p];
     blk0 = P.blk0;
     nblk = P.nblk;
     base = P.offset + first;
   }
-  const bool leader = finalize || ((int)blockIdx.x == blk0);
+  const bool leader = (int)blockIdx.x == blk0;
 
-  // Prefetch this lane's first chunk of every plane: the loads do not depend on the pose, so
-  // their latency overlaps the prologue below.
-  float xs[VEC], ys[VEC], zs[VEC], us[VEC], vs[VEC];
-#pragma unroll
-  for (int k = 0; k < VEC; ++k) xs[k] = ys[k] = zs[k] = us[k] = vs[k] = 0.0f;
+  // Items per lane per step: VEC = 4 -> a float4 of 4 consecutive items; VEC = 1 -> items c and
+  // c + PICP_BLOCK (coalesced across the block).  Processed in pairs (accumulate2).
+  constexpr int NI = (VEC == 4) ? 4 : 2;
+  constexpr int ISTRIDE = (VEC == 4) ? 1 : PICP_BLOCK;  // distance between a lane's items
+  constexpr int STEP = PICP_BLOCK * NI;
   const int c0 = tid * VEC;
-  if (!finalize && c0 < count) {
+  // load the step at c < count.  VEC = 4: the float4 at c stays inside the problem's padded
+  // range (offsets and block ranges are multiples of 4); VEC = 1: an item past `count` reads a
+  // clamped valid item.  Items past `count` are masked by accumulate2.
+  auto load_step = [&](int c, float* lx, float* ly, float* lz, float* lu, float* lv) {
     if constexpr (VEC == 4) {
-      const float4 x4 = *reinterpret_cast<const float4*>(X + base + c0);
-      const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c0);
-      const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c0);
-      const float4 u4 = *reinterpret_cast<const float4*>(U + base + c0);
-      const float4 v4 = *reinterpret_cast<const float4*>(V + base + c0);
-      xs[0] = x4.x; xs[1] = x4.y; xs[2] = x4.z; xs[3] = x4.w;
-      ys[0] = y4.x; ys[1] = y4.y; ys[2] = y4.z; ys[3] = y4.w;
-      zs[0] = z4.x; zs[1] = z4.y; zs[2] = z4.z; zs[3] = z4.w;
-      us[0] = u4.x; us[1] = u4.y; us[2] = u4.z; us[3] = u4.w;
-      vs[0] = v4.x; vs[1] = v4.y; vs[2] = v4.z; vs[3] = v4.w;
+      const float4 x4 = *reinterpret_cast<const float4*>(X + base + c);
+      const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c);
+      const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c);
+      const float4 u4 = *reinterpret_cast<const float4*>(U + base + c);
+      const float4 v4 = *reinterpret_cast<const float4*>(V + base + c);
+      lx[0] = x4.x; lx[1] = x4.y; lx[2] = x4.z; lx[3] = x4.w;
+      ly[0] = y4.x; ly[1] = y4.y; ly[2] = y4.z; ly[3] = y4.w;
+      lz[0] = z4.x; lz[1] = z4.y; lz[2] = z4.z; lz[3] = z4.w;
+      lu[0] = u4.x; lu[1] = u4.y; lu[2] = u4.z; lu[3] = u4.w;
+      lv[0] = v4.x; lv[1] = v4.y; lv[2] = v4.z; lv[3] = v4.w;
     } else {
-      xs[0] = X[base + c0];
-      ys[0] = Y[base + c0];
-      zs[0] = Z[base + c0];
-      us[0] = U[base + c0];
-      vs[0] = V[base + c0];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) {
+        const int ck = min(c + k * ISTRIDE, max(count - 1, 0));
+        lx[k] = X[base + ck];
+        ly[k] = Y[base + ck];
+        lz[k] = Z[base + ck];
+        lu[k] = U[base + ck];
+        lv[k] = V[base + ck];
+      }
     }
-  }
+  };
+  // Streaming (VEC = 4): a ring of RING register slots, slot s holding the step at
+  // c + s*STEP; each slot's next step is loaded as soon as the slot has been consumed, so every
+  // wave keeps RING-1 steps of HBM reads in flight while it computes (memory-level parallelism
+  // beyond the 2 resident waves per SIMD).  Single frames (VEC = 1) are latency-bound: one slot.
+  constexpr int RING = (VEC == 4) ? 3 : 1;
+  float bx[RING][NI], by[RING][NI], bz[RING][NI], bu[RING][NI], bv[RING][NI];
+  // The first steps do not depend on the pose, so their latency overlaps the state read below.
+#pragma unroll
+  for (int sl = 0; sl < RING; ++sl)
+    if (c0 + sl * STEP < count) load_step(c0 + sl * STEP, bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
 
-  if (j == 0) {
-    if (tid < 12) s_pose[tid] = (tid < 9) ? st_in[p].R[tid] : st_in[p].t[tid - 9];
-    if (tid == 0) {
-      PicpState s = st_in[p];
-      s.chi_prev = FLT_MAX;  // exec/icp_test.cpp:89
-      s.chi_in = s.chi_out = 0.0f;
-      s.n_in = s.n_proj = 0;
-      s.rounds = 0;
-      s.done = (A.max_rounds <= 0) ? 1 : 0;
-      s.ok = 1;
-      s.converged = 0;
-      if (leader) st_out[p] = s;
-      s_go = !s.done;
-    }
-  } else {
-    // The state (128 B -> LDS) and the previous round's partials are independent loads: issue
-    // both before waiting on either.  The partials of a finished problem are stale but unused.
-    int32_t st_word = 0;
-    if (tid < 32) st_word = reinterpret_cast<const int32_t*>(st_in + p)[tid];
-    STAMP(1);
-    reduce_partials(part_in, blk0, nblk, s_red, s_tot, tid < 32 ? &s_state[tid] : nullptr, st_word);
-    STAMP(2);
-    const PicpState& s_in = *reinterpret_cast<const PicpState*>(s_state);
-    if (s_in.done) {  // finished earlier: propagate the state through the ping-pong
-      if (leader && tid < 32) reinterpret_cast<int32_t*>(&st_out[p])[tid] = s_state[tid];
-      return;
-    }
-    if (tid == 0) {
-      double tot[PICP_NPART];
-#pragma unroll
-      for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
-      PicpState ns;
-      finish_round(A, s_in, tot, j, ns);
-      STAMP(6);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
-      s_go = !ns.done;
-      if (leader) st_out[p] = ns;
-    }
+  if (tid < 32) s_state[tid] = reinterpret_cast<const int32_t*>(st_in + p)[tid];
+  __syncthreads();
+  if (j == 0 && tid == 0) {  // the icp_test loop state at entry (exec/icp_test.cpp:89)
+    PicpState& s = *reinterpret_cast<PicpState*>(s_state);
+    s.chi_prev = FLT_MAX;
+    s.chi_in = s.chi_out = 0.0f;
+    s.n_in = s.n_proj = 0;
+    s.rounds = 0;
+    s.done = (A.max_rounds <= 0) ? 1 : 0;
+    s.ok = 1;
+    s.converged = 0;
   }
   __syncthreads();
-  STAMP(3);
-  if (finalize || !s_go) return;
+  STAMP(1);
+  const PicpState& s_in = *reinterpret_cast<const PicpState*>(s_state);
+  if (s_in.done) {  // finished earlier: propagate the state through the ping-pong
+    if (leader && tid < 32) reinterpret_cast<int32_t*>(&st_out[p])[tid] = s_state[tid];
+    return;
+  }
 
   // ---------------- linearize (src/picp_solver.cpp:56-91) ----------------
   Pose T;
-  T.r00 = s_pose[0]; T.r10 = s_pose[1]; T.r20 = s_pose[2];
-  T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
-  T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
-  T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
+  T.r00 = s_in.R[0]; T.r10 = s_in.R[1]; T.r20 = s_in.R[2];
+  T.r01 = s_in.R[3]; T.r11 = s_in.R[4]; T.r21 = s_in.R[5];
+  T.r02 = s_in.R[6]; T.r12 = s_in.R[7]; T.r22 = s_in.R[8];
+  T.t0 = s_in.t[0]; T.t1 = s_in.t[1]; T.t2 = s_in.t[2];
   Cam C;
   C.k00 = A.K[0]; C.k10 = A.K[1]; C.k20 = A.K[2];
   C.k01 = A.K[3]; C.k11 = A.K[4]; C.k21 = A.K[5];
@@ -226,61 +214,71 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   C.maxx = A.maxx;
   C.maxy = A.maxy;
   const float thr = A.threshold;
+  const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
 
-  Acc a;
+  Acc2 a;
+  acc2_zero(a);
+  for (int c = c0; c < count; c += RING * STEP) {
 #pragma unroll
-  for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
+    for (int sl = 0; sl < RING; ++sl) {
+      const int cs = c + sl * STEP;
+      if (cs < count) {
 #pragma unroll
-  for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
-  a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
-
-  for (int c = c0; c < count; c += PICP_BLOCK * VEC) {
-    if (c != c0) {  // chunks after the prefetched one
-      if constexpr (VEC == 4) {
-        const float4 x4 = *reinterpret_cast<const float4*>(X + base + c);
-        const float4 y4 = *reinterpret_cast<const float4*>(Y + base + c);
-        const float4 z4 = *reinterpret_cast<const float4*>(Z + base + c);
-        const float4 u4 = *reinterpret_cast<const float4*>(U + base + c);
-        const float4 v4 = *reinterpret_cast<const float4*>(V + base + c);
-        xs[0] = x4.x; xs[1] = x4.y; xs[2] = x4.z; xs[3] = x4.w;
-        ys[0] = y4.x; ys[1] = y4.y; ys[2] = y4.z; ys[3] = y4.w;
-        zs[0] = z4.x; zs[1] = z4.y; zs[2] = z4.z; zs[3] = z4.w;
-        us[0] = u4.x; us[1] = u4.y; us[2] = u4.z; us[3] = u4.w;
-        vs[0] = v4.x; vs[1] = v4.y; vs[2] = v4.z; vs[3] = v4.w;
-      } else {
-        xs[0] = X[base + c];
-        ys[0] = Y[base + c];
-        zs[0] = Z[base + c];
-        us[0] = U[base + c];
-        vs[0] = V[base + c];
+        for (int k = 0; k < NI; k += 2)
+          accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){bx[sl][k], bx[sl][k + 1]},
+                          (f2){by[sl][k], by[sl][k + 1]}, (f2){bz[sl][k], bz[sl][k + 1]},
+                          (f2){bu[sl][k], bu[sl][k + 1]}, (f2){bv[sl][k], bv[sl][k + 1]},
+                          cs + k * ISTRIDE < count, cs + (k + 1) * ISTRIDE < count, a);
+        const int cn = cs + RING * STEP;
+        if (cn < count) load_step(cn, bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
       }
     }
-    const int rem = count - c;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], rem > k, a);
   }
 
-  STAMP(4);
+  STAMP(2);
   float v[PICP_NPART];
-#pragma unroll
-  for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
-  v[PICP_P_CHI_IN] = a.chi_in;
-  v[PICP_P_CHI_OUT] = a.chi_out;
-  v[PICP_P_N_IN] = a.n_in;
-  v[PICP_P_N_PROJ] = a.n_proj;
-  v[31] = 0.0f;
+  acc2_fold(a, v);
   const int lane = tid & 63, wave = tid >> 6;
   const float wsum = wave_reduce32(v, lane);
   if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
   __syncthreads();
-  if (tid < PICP_NPART) {
-    float sum = s_wave[0][tid];
+  // publish: lane t < 16 of wave 0 stores partial floats (2t, 2t+1) as one write-through
+  // 8-byte word, the wave drains its stores, then lane 0 takes the problem's ticket
+  if (tid < 16) {
+    float e0 = s_wave[0][2 * tid], e1 = s_wave[0][2 * tid + 1];
 #pragma unroll
-    for (int w = 1; w < PICP_BLOCK / 64; ++w) sum += s_wave[w][tid];
-    part_out[(size_t)blockIdx.x * PICP_NPART + tid] = sum;
+    for (int w = 1; w < PICP_BLOCK / 64; ++w) {
+      e0 += s_wave[w][2 * tid];
+      e1 += s_wave[w][2 * tid + 1];
+    }
+    const unsigned long long word = ((unsigned long long)__float_as_uint(e1) << 32) | __float_as_uint(e0);
+    __hip_atomic_store(part + (size_t)blockIdx.x * (PICP_NPART / 2) + tid, word, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wave == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) {
+      const unsigned int old = __hip_atomic_fetch_add(tickets + p, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+      s_last = (old == (unsigned)(nblk - 1)) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+  if (!s_last) return;
+
+  // ---------------- the last arriver finishes the round (src/picp_solver.cpp:93-105) -------
+  reduce_published(part, blk0, nblk, s_red, s_tot);
+  STAMP(4);
+  if (tid == 0) {
+    double tot[PICP_NPART];
+#pragma unroll
+    for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
+    PicpState ns;
+    finish_round(A, s_in, tot, j + 1, ns);
+    st_out[p] = ns;
+    __hip_atomic_store(tickets + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   STAMP(5);
 }
@@ -335,17 +333,20 @@ extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, c
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const int4* blkinfo,
                                         const PicpState* st_in, PicpState* st_out,
-                                        const float* part_in, float* part_out, int j,
-                                        int finalize) {
-  if (grid <= 0 || !args) return hipErrorInvalidValue;
-  if (vec == 4)
-    hipLaunchKernelGGL(picp_round_kernel<4>, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U,
-                       V, *args, probs, blkinfo, st_in, st_out, part_in, part_out, j, finalize);
-  else if (vec == 1)
-    hipLaunchKernelGGL(picp_round_kernel<1>, dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U,
-                       V, *args, probs, blkinfo, st_in, st_out, part_in, part_out, j, finalize);
-  else
+                                        unsigned long long* part, unsigned int* tickets, int j) {
+  if (grid <= 0 || !args || !part || !tickets) return hipErrorInvalidValue;
+  const bool ph = picp_use_pinhole(args->K);
+#define PICP_LAUNCH_R(VEC, PH)                                                                        \
+  hipLaunchKernelGGL((picp_round_kernel<VEC, PH>), dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U, \
+                     V, *args, probs, blkinfo, st_in, st_out, part, tickets, j)
+  if (vec == 4) {
+    if (ph) PICP_LAUNCH_R(4, 1); else PICP_LAUNCH_R(4, 0);
+  } else if (vec == 1) {
+    if (ph) PICP_LAUNCH_R(1, 1); else PICP_LAUNCH_R(1, 0);
+  } else {
     return hipErrorInvalidValue;
+  }
+#undef PICP_LAUNCH_R
   return hipGetLastError();
 }
 

@@ -51,7 +51,7 @@ __device__ __forceinline__ bool timed_out(unsigned long long deadline) {
   return __builtin_amdgcn_s_memrealtime() > deadline;
 }
 
-template <int NPT>
+template <int NPT, int PH>
 __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
@@ -121,6 +121,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
   C.maxx = A.maxx;
   C.maxy = A.maxy;
   const float thr = A.threshold;
+  const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
 
   for (unsigned epoch = 1; !s_done; ++epoch) {
@@ -131,25 +132,34 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
     T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
-    Acc a;
-#pragma unroll
-    for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
-    a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k)
-      accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], tid + k * PICP_PBLOCK < count, a);
     float v[PICP_NPART];
+    if constexpr (NPT == 1) {  // one item per lane: the scalar path (latency-bound C2 frames)
+      Acc a;
 #pragma unroll
-    for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
+      for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
-    v[PICP_P_CHI_IN] = a.chi_in;
-    v[PICP_P_CHI_OUT] = a.chi_out;
-    v[PICP_P_N_IN] = a.n_in;
-    v[PICP_P_N_PROJ] = a.n_proj;
-    v[31] = 0.0f;
+      for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
+      a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
+      accumulate<PH>(T, C, thr, inv_thr, keep, xs[0], ys[0], zs[0], us[0], vs[0], tid < count, a);
+#pragma unroll
+      for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
+      v[PICP_P_CHI_IN] = a.chi_in;
+      v[PICP_P_CHI_OUT] = a.chi_out;
+      v[PICP_P_N_IN] = a.n_in;
+      v[PICP_P_N_PROJ] = a.n_proj;
+      v[31] = 0.0f;
+    } else {  // pairs of register-resident items, packed (accumulate2)
+      Acc2 a;
+      acc2_zero(a);
+#pragma unroll
+      for (int k = 0; k < NPT; k += 2)
+        accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k + 1]}, (f2){ys[k], ys[k + 1]},
+                        (f2){zs[k], zs[k + 1]}, (f2){us[k], us[k + 1]}, (f2){vs[k], vs[k + 1]},
+                        tid + k * PICP_PBLOCK < count, tid + (k + 1) * PICP_PBLOCK < count, a);
+      acc2_fold(a, v);
+    }
     const float wsum = wave_reduce32(v, lane);
     if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
     __syncthreads();
@@ -267,9 +277,14 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              unsigned long long* gpart, unsigned long long* gpose,
                                              unsigned int* err, unsigned long long timeout_ticks) {
   if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
-#define PICP_LAUNCH_P(N)                                                                             \
-  hipLaunchKernelGGL(picp_persistent_kernel<N>, dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, U, \
-                     V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks)
+  const bool ph = picp_use_pinhole(args->K);
+#define PICP_LAUNCH_P(N)                                                                                 \
+  if (ph)                                                                                                \
+    hipLaunchKernelGGL((picp_persistent_kernel<N, 1>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
+                       U, V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks);                   \
+  else                                                                                                   \
+    hipLaunchKernelGGL((picp_persistent_kernel<N, 0>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
+                       U, V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks)
   switch (npt) {
     case 1: PICP_LAUNCH_P(1); break;
     case 2: PICP_LAUNCH_P(2); break;

@@ -1,8 +1,8 @@
 // picp_runtime.cpp -- host runtime behind the C-ABI (include/picp_c.h).
 //
 // Owns device memory, the HIP stream of each handle, the block partition of a batch and the
-// hipGraph that replays the fused R-round solve (1 memcpy node + R linearize launches +
-// 1 finalize launch).  No torch, no host fallback: every compute entry point runs the HIP
+// hipGraph that replays the fused R-round solve (graph mode: 1 memcpy node + 1 ticket memset
+// node + R round launches, each finished in-launch by its last arriving block).  No torch, no host fallback: every compute entry point runs the HIP
 // kernels of picp_kernels.hip or fails with PICP_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 
@@ -26,8 +26,7 @@ extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, c
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const int4* blkinfo,
                                         const PicpState* st_in, PicpState* st_out,
-                                        const float* part_in, float* part_out, int j,
-                                        int finalize);
+                                        unsigned long long* part, unsigned int* tickets, int j);
 extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int npt, const float* X,
                                              const float* Y, const float* Z, const float* U,
                                              const float* V, const PicpArgs* args,
@@ -151,7 +150,8 @@ struct picp_batch {
   int4* blk_d = nullptr;
   PicpState* init_d = nullptr;
   PicpState* st_d[2] = {nullptr, nullptr};
-  float* part_d[2] = {nullptr, nullptr};
+  unsigned long long* part_d = nullptr;  // graph mode: published block partials (16 words each)
+  unsigned int* tickets_d = nullptr;     // graph mode: per-problem arrival tickets
   PicpState* st_pinned = nullptr;  // np_cap states
   std::vector<PicpState> init_h;
   std::vector<PicpState> result_h;
@@ -202,7 +202,10 @@ static int items_per_block(int64_t total) {
   // Large batches (HBM streaming): float4 per lane and several chunks per lane to amortise the
   // block reduction and the partial traffic.
   if (total <= ((int64_t)1 << 18)) return 2 * PICP_BLOCK;  // measured best for C2 (tools/sweep.py)
-  if (total >= (int64_t)8 << 20) return PICP_BLOCK * 4 * 4;
+  // streaming: about two resident 256-thread blocks per CU (all blocks in flight at once),
+  // each streaming its slice through the prefetch ring (profiles/r01/sweep_*m_*.log)
+  if (total >= (int64_t)8 << 20) return PICP_BLOCK * 4 * 32;
+  if (total >= (int64_t)2 << 20) return PICP_BLOCK * 4 * 8;
   return PICP_BLOCK * 4 * 2;
 }
 
@@ -306,13 +309,18 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
   }
   if (nblk > b->nblk_cap) {
     if (b->blk_d) hipFree(b->blk_d);
-    for (int k = 0; k < 2; ++k) if (b->part_d[k]) hipFree(b->part_d[k]);
-    b->blk_d = nullptr; b->part_d[0] = b->part_d[1] = nullptr;
+    if (b->part_d) hipFree(b->part_d);
+    b->blk_d = nullptr;
+    b->part_d = nullptr;
     HIP_TRY(hipMalloc(&b->blk_d, (size_t)nblk * sizeof(int4)));
-    for (int k = 0; k < 2; ++k) HIP_TRY(hipMalloc(&b->part_d[k], (size_t)nblk * PICP_NPART * sizeof(float)));
+    HIP_TRY(hipMalloc(&b->part_d, (size_t)nblk * (PICP_NPART / 2) * sizeof(unsigned long long)));
     b->nblk_cap = nblk;
   }
   if (np > b->np_cap) {
+    if (b->tickets_d) hipFree(b->tickets_d);
+    b->tickets_d = nullptr;
+    HIP_TRY(hipMalloc(&b->tickets_d, (size_t)np * sizeof(unsigned int)));
+    HIP_TRY(hipMemsetAsync(b->tickets_d, 0, (size_t)np * sizeof(unsigned int), b->stream));
     if (b->probs_d) hipFree(b->probs_d);
     if (b->init_d) hipFree(b->init_d);
     for (int k = 0; k < 2; ++k) if (b->st_d[k]) hipFree(b->st_d[k]);
@@ -362,6 +370,9 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
   for (int i = 0; i < np; ++i) {
     memset(&b->init_h[i], 0, sizeof(PicpState));
     b->init_h[i].R[0] = b->init_h[i].R[4] = b->init_h[i].R[8] = 1.0f;
+    // the loop state at entry (what a zero-round solve returns; the kernels set it again)
+    b->init_h[i].chi_prev = FLT_MAX;
+    b->init_h[i].ok = 1;
   }
   HIP_TRY(hipMemcpyAsync(b->init_d, b->init_h.data(), (size_t)np * sizeof(PicpState), hipMemcpyHostToDevice, b->stream));
   b->result_h.assign(np, PicpState{});
@@ -399,13 +410,27 @@ static int batch_upload_params(picp_batch* b, const picp_params* prm) {
   return PICP_OK;
 }
 
-static hipError_t launch_round(picp_batch* b, int j, int fin, int in_buf) {
-  return picp_launch_round(b->stream, fin ? b->np : b->nblk, b->vec, b->X(), b->Y(), b->Z(), b->U(),
-                           b->V(), &b->args, b->probs_d, b->blk_d, b->st_d[in_buf], b->st_d[in_buf ^ 1],
-                           b->part_d[in_buf], b->part_d[in_buf ^ 1], j, fin);
+// graph mode: launch j reads st_d[(j+1)&1] and its last arrivers write st_d[j&1]; the initial
+// states go to st_d[1], so after R launches the result is in st_d[(R-1)&1] (st_d[1] if R == 0)
+static hipError_t launch_round(picp_batch* b, int j) {
+  const int in_buf = (j + 1) & 1;
+  return picp_launch_round(b->stream, b->nblk, b->vec, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
+                           b->probs_d, b->blk_d, b->st_d[in_buf], b->st_d[in_buf ^ 1], b->part_d,
+                           b->tickets_d, j);
 }
 
-// Enqueue the R+1 launches (plus the initial-state copy) of a fused solve on the stream.
+static int graph_result_idx(int R) { return R >= 1 ? ((R - 1) & 1) : 1; }
+
+// graph-mode prologue of every solve: initial states in, arrival tickets zeroed
+static hipError_t graph_prologue(picp_batch* b) {
+  hipError_t e = hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState),
+                                hipMemcpyDeviceToDevice, b->stream);
+  if (e != hipSuccess) return e;
+  return hipMemsetAsync(b->tickets_d, 0, (size_t)b->np * sizeof(unsigned int), b->stream);
+}
+
+// Enqueue a fused R-round solve on the stream: block / persistent mode one launch; graph mode
+// the initial-state copy, the ticket memset and R round launches.
 static hipError_t enqueue_solve(picp_batch* b, int R) {
   if (b->mode == PICP_MODE_BLOCK)
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
@@ -420,11 +445,10 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
     return picp_launch_persistent(b->stream, b->nblk, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(),
                                   &b->args, b->init_d, b->st_d[0], gpart, gpose, err, b->timeout_ticks);
   }
-  hipError_t e = hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState),
-                                hipMemcpyDeviceToDevice, b->stream);
+  hipError_t e = graph_prologue(b);
   if (e != hipSuccess) return e;
-  for (int j = 0; j <= R; ++j) {
-    e = launch_round(b, j, (j == R) ? 1 : 0, (j + 1) & 1);
+  for (int j = 0; j < R; ++j) {
+    e = launch_round(b, j);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -454,7 +478,7 @@ static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   if (rc) return rc;
   HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
   b->last_rounds = R;
-  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? (R & 1) : 0;
+  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
   b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
   return PICP_OK;
 }
@@ -516,10 +540,10 @@ extern "C" int picp_batch_destroy(picp_batch_t* b) {
   if (b->blk_d) hipFree(b->blk_d);
   if (b->probs_d) hipFree(b->probs_d);
   if (b->init_d) hipFree(b->init_d);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 2; ++k)
     if (b->st_d[k]) hipFree(b->st_d[k]);
-    if (b->part_d[k]) hipFree(b->part_d[k]);
-  }
+  if (b->part_d) hipFree(b->part_d);
+  if (b->tickets_d) hipFree(b->tickets_d);
   if (b->st_pinned) hipHostFree(b->st_pinned);
   if (b->sync) hipFree(b->sync);
   if (b->stream) hipStreamDestroy(b->stream);
@@ -636,7 +660,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
   HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
   if (total_ms) *total_ms = ms;
   b->last_rounds = R;
-  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? (R & 1) : 0;
+  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
   b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
   if (kernel_us) {
     // [0]: mean launch period of the round kernel inside the replayed graphs (event time over
@@ -644,7 +668,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
     //      the per-launch duration a kernel trace reports);
     // [1]: mean of event pairs around single launches of the same solve (an upper bound: it
     //      adds the event overhead to every launch).
-    const int launches = (b->mode == PICP_MODE_GRAPH) ? (R + 1) : 1;
+    const int launches = (b->mode == PICP_MODE_GRAPH) ? std::max(R, 1) : 1;
     kernel_us[0] = 1000.0f * ms / (float)(reps * launches);
     if (b->mode != PICP_MODE_GRAPH) {
       hipEvent_t a0, a1;
@@ -665,17 +689,17 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
       b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
       return batch_read_results(b);
     }
-    std::vector<hipEvent_t> ev((size_t)(R + 2));
+    std::vector<hipEvent_t> ev((size_t)(R + 1));
     for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
     double lin_us = 0.0;
     int lin_n = 0;
-    HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, (size_t)b->np * sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
-    for (int j = 0; j <= R; ++j) {
+    HIP_TRY(graph_prologue(b));
+    for (int j = 0; j < R; ++j) {
       HIP_TRY(hipEventRecord(ev[j], b->stream));
-      HIP_TRY(launch_round(b, j, (j == R) ? 1 : 0, (j + 1) & 1));
+      HIP_TRY(launch_round(b, j));
     }
-    HIP_TRY(hipEventRecord(ev[R + 1], b->stream));
-    HIP_TRY(hipEventSynchronize(ev[R + 1]));
+    HIP_TRY(hipEventRecord(ev[R], b->stream));
+    HIP_TRY(hipEventSynchronize(ev[R]));
     for (int j = 0; j < R; ++j) {
       float t = 0.0f;
       HIP_TRY(hipEventElapsedTime(&t, ev[j], ev[j + 1]));
@@ -684,7 +708,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
     }
     for (auto& e : ev) hipEventDestroy(e);
     kernel_us[1] = lin_n ? (float)(lin_us / lin_n) : 0.0f;
-    b->result_idx = R & 1;
+    b->result_idx = graph_result_idx(R);
     b->last_persistent = false;
   }
   hipEventDestroy(e0);
@@ -873,11 +897,10 @@ extern "C" int picp_one_round(picp_t* h, float threshold, float damping, int min
   if (rc) return rc;
   rc = handle_upload_pose(h);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
-  HIP_TRY(launch_round(b, 0, 0, 1));
-  HIP_TRY(launch_round(b, 1, 1, 0));
+  HIP_TRY(graph_prologue(b));
+  HIP_TRY(launch_round(b, 0));
   b->last_rounds = 1;
-  b->result_idx = 1;
+  b->result_idx = graph_result_idx(1);
   b->last_persistent = false;
   rc = batch_read_results(b);
   if (rc) return rc;
@@ -921,10 +944,10 @@ extern "C" int picp_linearize(picp_t* h, float threshold, int keep_outliers, dou
   if (rc) return rc;
   rc = handle_upload_pose(h);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(b->st_d[1], b->init_d, sizeof(PicpState), hipMemcpyDeviceToDevice, b->stream));
-  HIP_TRY(launch_round(b, 0, 0, 1));
-  std::vector<float> part((size_t)b->nblk * PICP_NPART);
-  HIP_TRY(hipMemcpyAsync(part.data(), b->part_d[0], part.size() * sizeof(float), hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(graph_prologue(b));
+  HIP_TRY(launch_round(b, 0));
+  std::vector<float> part((size_t)b->nblk * PICP_NPART);  // the published words are float pairs
+  HIP_TRY(hipMemcpyAsync(part.data(), b->part_d, part.size() * sizeof(float), hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   double tot[PICP_NPART] = {0};
   for (int k = 0; k < b->nblk; ++k)

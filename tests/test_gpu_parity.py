@@ -22,6 +22,15 @@ POSE_TOL = 1e-4
 THR = 3000.0  # exec/icp_test.cpp:86
 
 
+def _pose_tol(n):
+    """1-2 correspondences under-determine the 6-DoF pose (rank(J^T J) <= 4): 50 damped rounds
+    amplify last-bit differences without bound in the unobservable directions -- the oracle's own
+    float32 and float64 accumulations of the same problem end 1e-4..4e-4 apart, and a bit-exact
+    Jacobian does not change that (tools/k_paths.py).  Those cases are held to 1e-2; every
+    determined problem (n >= 3) to the north-star 1e-4."""
+    return POSE_TOL if n >= 3 else 1e-2
+
+
 def _synth():
     from picp_amd import synth
     return synth
@@ -52,6 +61,30 @@ def test_linearize_matches_oracle(native, oracle, n, seed, of, noise, keep):
     assert got["n_in"] == ref["n_in"]
     assert got["n_projected"] == ref["n_projected"]
     _lin_close(got, ref)
+
+
+@pytest.mark.parametrize("n", [1000, 100003])
+@pytest.mark.parametrize("keep", [0, 1])
+def test_general_camera_path_matches_oracle(native, oracle, n, keep):
+    """A K that is not [fx 0 cx; 0 fy cy; 0 0 1] (skew, and a non-unit K(2,2)) runs the general
+    projection path (accumulate_one); the reference's pinhole K runs the specialised one.  Both
+    are held to the same gate exactness and H/b tolerance."""
+    synth = _synth()
+    p = synth.make_problem(n, seed=5, outlier_frac=0.2, pixel_noise=0.5)
+    K = np.array([[180, 3.5, 320], [0, 181, 240], [0, 0, 1.0000001]], np.float32)
+    s = native.PICPSolver(rows=480, cols=640, K=K)
+    s.init(p["T_init"], p["world"], p["image"])
+    s.setKernelThreshold(THR)
+    got = s.linearize(p["pairs"], keep_outliers=bool(keep))
+    ref = oracle.linearize(p["T_init"], K, 480, 640, p["world"], p["image"], p["pairs"], THR,
+                           keep_outliers=keep, mode=oracle.MODE_F64)
+    assert got["n_in"] == ref["n_in"] and got["n_projected"] == ref["n_projected"]
+    _lin_close(got, ref)
+    st = s.solve(p["pairs"], max_rounds=20, conv_eps=-1.0, keep_outliers=bool(keep))
+    T_ref, _ = oracle.solve(p["T_init"], K, 480, 640, p["world"], p["image"], p["pairs"], THR,
+                            keep_outliers=bool(keep), max_rounds=20, conv_eps=-1.0)
+    assert synth.se3_log_norm(s.pose(), T_ref) < POSE_TOL
+    assert st["rounds"] == 20
 
 
 def test_linearize_matches_golden_vectors(native):
@@ -198,7 +231,7 @@ def test_batch_ragged_matches_single_and_oracle(native, oracle, mode):
         T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"][:n], p["y"][:n],
                                          p["z"][:n], p["u"][:n], p["v"][:n], THR,
                                          mode=oracle.MODE_F64, max_rounds=50, conv_eps=-1.0)
-        assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL, i
+        assert synth.se3_log_norm(poses[i], T_ref) < _pose_tol(n), (i, n)
         assert stats[i]["rounds"] == 50
         assert abs(stats[i]["n_in"] - st_ref["n_in"]) <= 2
         if n >= 1000 and mode == "graph":
@@ -353,7 +386,7 @@ def test_persistent_and_graph_modes_agree_with_oracle(native, oracle, n, of, kee
                                      THR, keep_outliers=keep, mode=oracle.MODE_F64, max_rounds=50,
                                      conv_eps=conv)
     for mode, (T, st) in res.items():
-        assert synth.se3_log_norm(T, T_ref) < POSE_TOL, mode
+        assert synth.se3_log_norm(T, T_ref) < _pose_tol(n), mode
         assert abs(st["n_in"] - st_ref["n_in"]) <= max(2, n // 100000), mode
         if conv < 0:
             assert st["rounds"] == 50
