@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="c5: sequence length (default 10000)")
     ap.add_argument("--obs", type=int, default=0, help="c5: observations per frame (default 2000)")
     ap.add_argument("--seg-len", type=int, default=40, help="c5: PICP steps per segment")
+    ap.add_argument("--stream-n", type=int, default=16000000,
+                    help="c2: also measure one streaming single frame of this many correspondences "
+                         "(roofline_streaming; 0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,12 +184,40 @@ def main():
         },
         "pose_err_vs_gt_se3": err,
     }
+    if args.workload == "c2" and args.stream_n > 0 and world == 1:
+        out["roofline_streaming"] = streaming_roofline(args.stream_n, R, thr, local if world > 1 else 0)
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(xyz[: sizes[0]], uv[: sizes[0]], T_init[0], R, thr, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def streaming_roofline(n, R, thr, device):
+    """The same solve on one frame large enough to stream from HBM every round (SURVEY.md §8d:
+    a > 256 MB working set, past the 256 MB Infinity Cache): 20 B x n per round-launch of
+    picp_round_kernel.  Reported beside the C2 line, whose single 100k frame is latency-bound."""
+    import picp_amd
+    from picp_amd import synth
+    p = synth.make_problem(n, seed=7, pixel_noise=0.5, shuffle=False)
+    b = picp_amd.Batch([n], device=device)
+    b.set_data(p["xyz"], p["uv"])
+    b.set_poses(p["T_init"][None])
+    params = dict(threshold=thr, max_rounds=R, conv_eps=-1.0)
+    b.solve(**params)
+    ev_ms, (launch_us, _) = b.time(5, **params)
+    info = b.info()
+    launches = 1 if info["mode"] == "graph" else 0
+    per_launch = BYTES_PER_CORR * n * (1 if launches else R)
+    achieved = per_launch / (launch_us * 1e-6) / 1e9
+    err = synth.se3_log_norm(b.poses()[0], p["T_gt"])
+    return {"bound": "hbm", "n_corr": n, "working_set_MB": round(BYTES_PER_CORR * n / 1e6, 1),
+            "kernel": "picp_round_kernel (one GN round per launch)" if launches else info["mode"],
+            "mode": info["mode"], "blocks_per_launch": info["n_blocks"], "kernel_us": round(launch_us, 3),
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "iterations_per_s": round(R * 5 / (ev_ms * 1e-3), 2),
+            "pose_err_vs_gt_se3": err}
 
 
 def bench_vo(args, wl, world, rank, local, dist, torch):
