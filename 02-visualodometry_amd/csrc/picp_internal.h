@@ -125,4 +125,12 @@ struct VoArgs {     // by value; every pointer is device memory
   float* poses;              // 16 per slot, camera-in-world, column-major
   VoStep* steps;
   int2* pairs;               // append scratch: segment s at s * cap_c
+  // matcher prep (picp_match.hip): fp16 rows of dp = 16*kch halves + two guard norms
+  int32_t dp;
+  const _Float16* obs_h;
+  const float* obs_n1;
+  const float* obs_n2;
+  _Float16* map_h;
+  float* map_n1;
+  float* map_n2;
 };

@@ -16,6 +16,7 @@
 
 #include <float.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "picp_internal.h"
 
@@ -29,12 +30,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 // The reference's update (src/my_utilities.h:91-97), in index order,
 //   if (d < best) { second = best; best = d; bi = j; } else if (d < second) second = d;
-// branch-free for finite d >= 0 (best <= second always holds):
+// branch-free for d >= 0 or NaN (best <= second always holds; NaN is mapped to +inf, which
+// leaves all three unchanged exactly as the reference's comparisons do):
 //   second' = med3(best, d, second)   (d < best: best; best <= d < second: d; else second;
 //                                       d == best: best == d, as the reference's else-branch)
 //   best'   = d < best ? d : best
 //   bi'     = d < best ? j : bi       (strict: the first index of the minimum wins)
 __device__ inline void match_update(float d, int32_t j, float& best, float& second, int32_t& bi) {
+  d = fminf(d, INFINITY);  // a NaN distance never updates anything: make it +inf (IEEE minNum)
   const bool lt = d < best;
   second = __builtin_amdgcn_fmed3f(best, d, second);
   best = lt ? d : best;
@@ -106,6 +109,332 @@ __global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(
     second_dist[o] = second_b;
     accepted[o] = (bi_b != -1 && best_b < dist_thr && best_b / second_b < ratio_thr) ? 1 : 0;
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// MFMA pre-filter + exact rescan (same results, bit for bit).
+//
+// Pass 1: D'(q, r) = |r|^2 - 2 q.r from v_mfma_f32_32x32x16_f16 (fp16 operands, fp32
+// accumulation) -- the approximate distance minus the query's constant |q|^2 -- and per query
+// the approximate second-smallest s' over all references.  With D = |q|^2 + D' and d the
+// reference's float distance (sum of (q_k - r_k)^2 in order), |D - d| <= E_q for every safe
+// pair, where (v = 2^-11 fp16 rounding, u = 2^-24)
+//   E_q = 1.5 * [(2v + v^2 + 56u)(|q|^2 + Rmax) + 2^-22 (1 + |q|^2 + Rmax)]
+// (fp16 quantisation of both operands incl. subnormals, the fp32 accumulation, the fp32 norms,
+// the reference's own 12 roundings; 1.5x headroom).  Then every reference that can be the
+// exact best or second of q has D' <= s' + 2 E_q: the two smallest-D references have exact
+// d <= s' + |q|^2 + E_q, so the exact second s <= s'+|q|^2+E_q, and any r with d_r <= s has
+// D'_r <= d_r - |q|^2 + E_q <= s' + 2 E_q.
+// Pass 2: the references under that bound ("candidates", typically 2-4) are collected per
+// query; the exact update of the reference then runs over them in index order, which yields the
+// same best index (first minimum), best and second as scanning all of them.  A query with more
+// than MM_CAP candidates, a non-finite or |x| > 60000 component (fp16 range), or < 2 safe
+// references takes the exact full scan; an unsafe reference is a candidate for every query.
+// ---------------------------------------------------------------------------------------
+extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
+                                        const float* q_desc, const float* r_desc,
+                                        const MatchProblem* probs, int dim, float dist_thr,
+                                        float ratio_thr, int32_t* best_idx, float* best_dist,
+                                        float* second_dist, int32_t* accepted);
+
+typedef _Float16 mm_half8 __attribute__((ext_vector_type(8)));
+typedef float mm_f16v __attribute__((ext_vector_type(16)));
+
+#define MM_BLOCK 256
+#define MM_WAVES 4
+#define MM_RB 1                   // 32-query MFMA row blocks per wave (share every B operand)
+#define MM_QPW (32 * MM_RB)       // queries per wave
+#define MM_QPB (MM_WAVES * MM_QPW)
+#define MM_CAP 16                 // candidate slots per query
+#define MM_SAFE 60000.0f
+
+__device__ __forceinline__ float mm_bound(float nq, float rmax) {
+  const float v = 1.0f / 2048.0f, u = 1.0f / 16777216.0f;
+  const float t = nq + rmax;
+  return 1.5f * ((2.0f * v + v * v + 56.0f * u) * t + (1.0f / 4194304.0f) * (1.0f + t));
+}
+
+// the reference's distance (src/my_utilities.h:83-90), exactly
+__device__ __forceinline__ float mm_exact_dist(const float* q, const float* __restrict__ r, int dim) {
+#pragma clang fp contract(off)
+  float d = 0.0f;
+  for (int k = 0; k < dim; ++k) {
+    const float t = q[k] - r[k];
+    d = d + t * t;
+  }
+  return d;
+}
+
+// Prep of n descriptors (float[dim] rows): fp16 rows padded to 16*kch, and the two guard norms
+//   n1 = |x|^2, +inf if a component is non-finite or beyond +-60000 (fp16 range): pass 1
+//   n2 = |x|^2, -inf for such a row: pass 2 (an unsafe reference is every query's candidate)
+// An unsafe row's fp16 values are zeroed so its MFMA products stay finite.
+extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc, int64_t n, int dim,
+                                                  int kch, _Float16* __restrict__ h,
+                                                  float* __restrict__ n1, float* __restrict__ n2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int dp = 16 * kch;
+  float nr = 0.0f;
+  bool bad = false;
+  for (int k = 0; k < dim; ++k) {
+    const float x = desc[i * dim + k];
+    bad |= !(fabsf(x) <= MM_SAFE);
+    nr = fmaf(x, x, nr);
+  }
+  for (int k = 0; k < dp; ++k) h[i * dp + k] = (_Float16)((k < dim && !bad) ? desc[i * dim + k] : 0.0f);
+  n1[i] = bad ? INFINITY : nr;
+  n2[i] = bad ? -INFINITY : nr;
+}
+
+// The pre-filter kernel.  q_*/r_* prep arrays are indexed like the fp32 descriptors.  The
+// references stream through LDS in tiles of MM_RT, double-buffered: one barrier per tile, the
+// next tile's 16-B rows fetched into registers while this one is computed.
+#define MM_RT 128
+template <int KCH>
+__global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
+    const float* __restrict__ q_desc, const float* __restrict__ r_desc,
+    const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
+    const _Float16* __restrict__ r_h, const float* __restrict__ r_n1, const float* __restrict__ r_n2,
+    const MatchProblem* __restrict__ probs, int dim, float dist_thr, float ratio_thr,
+    int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
+    float* __restrict__ second_dist, int32_t* __restrict__ accepted) {
+  constexpr int DP = 16 * KCH;                      // halves per prepped row
+  constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
+  constexpr int CPT = (CH + MM_BLOCK - 1) / MM_BLOCK;  // chunks per thread
+  constexpr int DMAX = 16 * KCH;
+  __shared__ mm_half8 s_t[2][CH];                   // tile rows, 16-B chunks: row*(DP/8) + c*2 + h
+  __shared__ float s_n[2][2][MM_RT];                // [buf][n1|n2][ref]
+  __shared__ int s_cnt[MM_WAVES][MM_QPW];
+  __shared__ int s_list[MM_WAVES][MM_QPW][MM_CAP];
+  __shared__ float s_nq[MM_WAVES][MM_QPW];
+
+  const MatchProblem P = probs[blockIdx.y];
+  const int64_t q0 = (int64_t)blockIdx.x * MM_QPB;
+  if (q0 >= P.nq) return;  // whole block past this problem
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int64_t qw = q0 + (int64_t)w * MM_QPW;  // this wave's first query
+
+  mm_half8 qa[MM_RB][KCH];  // A operands: query qw + 32 rb + r, halves [16c + 8 hf, +8)
+#pragma unroll
+  for (int rb = 0; rb < MM_RB; ++rb) {
+    const int64_t qi = min(qw + 32 * rb + r, P.nq - 1);
+#pragma unroll
+    for (int c = 0; c < KCH; ++c)
+      qa[rb][c] = *reinterpret_cast<const mm_half8*>(q_h + (P.q_off + qi) * DP + 16 * c + 8 * hf);
+  }
+  if (lane < MM_QPW) {
+    const int64_t qi = qw + lane;
+    s_nq[w][lane] = (qi < P.nq) ? q_n1[P.q_off + qi] : 0.0f;  // +inf: unsafe query
+    s_cnt[w][lane] = 0;
+  }
+
+  const int64_t nr_all = P.nr;
+  const mm_half8* rsrc = reinterpret_cast<const mm_half8*>(r_h + P.r_off * DP);
+  // register staging of one tile: CPT chunks + this thread's norms (threads < MM_RT)
+  mm_half8 st[CPT];
+  float sn1 = INFINITY, sn2 = INFINITY;
+  auto fetch = [&](int64_t t0) {
+    const int64_t nt = min((int64_t)MM_RT, nr_all - t0);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int ch = tid + k * MM_BLOCK;
+      const int64_t row = ch / (DP / 8);
+      st[k] = (ch < CH && row < nt) ? rsrc[t0 * (DP / 8) + ch] : mm_half8{};
+    }
+    if (tid < MM_RT) {
+      sn1 = (tid < nt) ? r_n1[P.r_off + t0 + tid] : INFINITY;  // past the end: excluded ...
+      sn2 = (tid < nt) ? r_n2[P.r_off + t0 + tid] : INFINITY;  // ... and never a candidate
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int ch = tid + k * MM_BLOCK;
+      if (ch < CH) s_t[buf][ch] = st[k];
+    }
+    if (tid < MM_RT) {
+      s_n[buf][0][tid] = sn1;
+      s_n[buf][1][tid] = sn2;
+    }
+  };
+
+  // ---------------- pass 1: an upper bound on the approximate second-best D' per row ----------
+  // Each lane keeps the minimum of D' over its own columns; the second-smallest of the 32 lane
+  // minima of a row is >= the row's true approximate second-best s' (equal unless the two
+  // smallest share a lane), so tau below can only be looser -- more candidates, same result.
+  float b1[MM_RB][16], s1[MM_RB][16];
+#pragma unroll
+  for (int rb = 0; rb < MM_RB; ++rb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b1[rb][i] = s1[rb][i] = INFINITY;
+  float rmax = 0.0f;
+  fetch(0);
+  stash(0);
+  int buf = 0;
+  for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
+    __syncthreads();                                 // tile t0 in s_t[buf]; s_t[buf^1] free
+    const bool more = t0 + MM_RT < nr_all;
+    if (more) fetch(t0 + MM_RT);
+#pragma unroll 1
+    for (int sub = 0; sub < MM_RT / 32; ++sub) {  // rolled: two accumulators live, not eight
+      const int col = sub * 32 + r;
+      mm_half8 bb[KCH];
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) bb[c] = s_t[buf][col * (DP / 8) + 2 * c + hf];
+      const float n1 = s_n[buf][0][col];
+      rmax = (n1 < INFINITY) ? fmaxf(rmax, n1) : rmax;
+#pragma unroll
+      for (int rb = 0; rb < MM_RB; ++rb) {
+        mm_f16v acc = {};
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bb[c], acc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) b1[rb][i] = fminf(b1[rb][i], fmaf(-2.0f, acc[i], n1));  // n1 = inf: excluded
+      }
+    }
+    if (more) stash(buf ^ 1);
+  }
+  // merge the 32 columns of each row (lanes with equal hf): top-2 of the union
+#pragma unroll
+  for (int m = 1; m < 32; m <<= 1) {
+#pragma unroll
+    for (int rb = 0; rb < MM_RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pb = __shfl_xor(b1[rb][i], m), ps = __shfl_xor(s1[rb][i], m);
+        s1[rb][i] = fminf(fmaxf(b1[rb][i], pb), fminf(s1[rb][i], ps));
+        b1[rb][i] = fminf(b1[rb][i], pb);
+      }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, m));
+  float tau[MM_RB][16];
+#pragma unroll
+  for (int rb = 0; rb < MM_RB; ++rb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+      tau[rb][i] = s1[rb][i] + 2.0f * mm_bound(s_nq[w][row], rmax);  // inf: every reference
+    }
+
+  // ---------------- pass 2: collect the candidates ----------------
+  __syncthreads();
+  fetch(0);
+  stash(0);
+  buf = 0;
+  for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
+    __syncthreads();
+    const bool more = t0 + MM_RT < nr_all;
+    if (more) fetch(t0 + MM_RT);
+#pragma unroll 1
+    for (int sub = 0; sub < MM_RT / 32; ++sub) {  // rolled: two accumulators live, not eight
+      const int col = sub * 32 + r;
+      mm_half8 bb[KCH];
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) bb[c] = s_t[buf][col * (DP / 8) + 2 * c + hf];
+      const float n2 = s_n[buf][1][col];  // -inf: forced candidate; +inf: past the end
+#pragma unroll
+      for (int rb = 0; rb < MM_RB; ++rb) {
+        mm_f16v acc = {};
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bb[c], acc, 0, 0, 0);
+        unsigned m = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m |= (fmaf(-2.0f, acc[i], n2) <= tau[rb][i]) ? (1u << i) : 0u;
+        while (m) {  // rare: the few candidates of this lane's 16 rows
+          const int i = __builtin_ctz(m);
+          m &= m - 1;
+          const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          const int slot = atomicAdd(&s_cnt[w][row], 1);
+          if (slot < MM_CAP) s_list[w][row][slot] = (int)(t0 + col);
+        }
+      }
+    }
+    if (more) stash(buf ^ 1);
+  }
+  __syncthreads();
+
+  // ---------------- exact update over the candidates, in index order ----------------
+  const int64_t qi = qw + lane;
+  if (lane < MM_QPW && qi < P.nq) {
+    float q[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) q[k] = (k < dim) ? q_desc[(P.q_off + qi) * dim + k] : 0.0f;
+    float best = FLT_MAX, second = FLT_MAX;  // :78-79
+    int32_t bi = -1;
+    const int n = s_cnt[w][lane];
+    if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) {  // slow path: the reference's full scan
+      for (int64_t j = 0; j < P.nr; ++j) {
+        const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
+        if (d < best) { second = best; best = d; bi = (int32_t)j; }
+        else if (d < second) second = d;
+      }
+    } else {
+      int idx[MM_CAP];
+#pragma unroll
+      for (int k = 0; k < MM_CAP; ++k) idx[k] = (k < n) ? s_list[w][lane][k] : 0x7fffffff;
+#pragma unroll
+      for (int a = 1; a < MM_CAP; ++a) {  // sort ascending (padding sorts last)
+#pragma unroll
+        for (int b = a; b > 0; --b) {
+          const int lo = min(idx[b - 1], idx[b]), hi = max(idx[b - 1], idx[b]);
+          idx[b - 1] = lo;
+          idx[b] = hi;
+        }
+      }
+      for (int k = 0; k < n; ++k) {
+        const int j = idx[k];
+        const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
+        if (d < best) { second = best; best = d; bi = j; }
+        else if (d < second) second = d;
+      }
+    }
+    const int64_t o = P.q_off + qi;
+    best_idx[o] = bi;
+    best_dist[o] = best;
+    second_dist[o] = second;
+    accepted[o] = (bi != -1 && best < dist_thr && best / second < ratio_thr) ? 1 : 0;  // :100-103
+  }
+}
+
+extern "C" int picp_match_prep_kch(int dim) { return dim <= 16 ? 1 : 2; }
+
+extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* desc, int64_t n, int dim,
+                                             _Float16* h, float* n1, float* n2) {
+  if (n <= 0) return hipSuccess;
+  if (dim < 1 || dim > PICP_MATCH_MAXD) return hipErrorInvalidValue;
+  const int threads = 256;
+  hipLaunchKernelGGL(picp_match_prep_kernel, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0,
+                     stream, desc, n, dim, picp_match_prep_kch(dim), h, n1, n2);
+  return hipGetLastError();
+}
+
+// The pre-filtered match over prepped descriptors (picp_launch_match_prep), unless
+// PICP_MATCH_EXACT=1 selects the exact scan (same results; for A/B checks).
+extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
+                                             const float* q_desc, const float* r_desc,
+                                             const _Float16* q_h, const float* q_n1,
+                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
+                                             const MatchProblem* probs, int dim, float dist_thr,
+                                             float ratio_thr, int32_t* best_idx, float* best_dist,
+                                             float* second_dist, int32_t* accepted) {
+  if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
+  if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
+  const char* ex = getenv("PICP_MATCH_EXACT");
+  if (ex && atoi(ex) != 0)
+    return picp_launch_match(stream, n_problems, max_nq, q_desc, r_desc, probs, dim, dist_thr, ratio_thr,
+                             best_idx, best_dist, second_dist, accepted);
+  const dim3 g((unsigned)((max_nq + MM_QPB - 1) / MM_QPB), (unsigned)n_problems);
+  if (dim <= 16)
+    hipLaunchKernelGGL(picp_match_mfma_kernel<1>, g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1,
+                       r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                       accepted);
+  else
+    hipLaunchKernelGGL(picp_match_mfma_kernel<2>, g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1,
+                       r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                       accepted);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,

@@ -45,6 +45,16 @@ extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int6
                                         const MatchProblem* probs, int dim, float dist_thr,
                                         float ratio_thr, int32_t* best_idx, float* best_dist,
                                         float* second_dist, int32_t* accepted);
+extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* desc, int64_t n, int dim,
+                                             _Float16* h, float* n1, float* n2);
+extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
+                                             const float* q_desc, const float* r_desc,
+                                             const _Float16* q_h, const float* q_n1,
+                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
+                                             const MatchProblem* probs, int dim, float dist_thr,
+                                             float ratio_thr, int32_t* best_idx, float* best_dist,
+                                             float* second_dist, int32_t* accepted);
+extern "C" int picp_match_prep_kch(int dim);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -1057,8 +1067,11 @@ extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1,
   const size_t b_probs = probs.size() * sizeof(MatchProblem);
   const size_t b_d1 = (size_t)n1 * dim * sizeof(float), b_d2 = (size_t)std::max<int64_t>(n2, 1) * dim * sizeof(float);
   const size_t b_out = (size_t)n1 * 4;
+  const int dp = 16 * picp_match_prep_kch(dim);
+  const size_t n2a = (size_t)std::max<int64_t>(n2, 1);
+  const size_t b_prep = ((size_t)n1 + n2a) * (dp * sizeof(_Float16) + 2 * sizeof(float));
   char* buf = nullptr;
-  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + 64));
+  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + 256));
   char* cur = buf;
   auto carve = [&](size_t bytes) { char* r = cur; cur += (bytes + 15) / 16 * 16; return r; };
   MatchProblem* d_probs = (MatchProblem*)carve(b_probs);
@@ -1068,11 +1081,20 @@ extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1,
   float* d_bd = (float*)carve(b_out);
   float* d_sd = (float*)carve(b_out);
   int32_t* d_acc = (int32_t*)carve(b_out);
+  _Float16* q_h = (_Float16*)carve((size_t)n1 * dp * sizeof(_Float16));
+  float* q_n1 = (float*)carve((size_t)n1 * 4);
+  float* q_n2 = (float*)carve((size_t)n1 * 4);
+  _Float16* r_h = (_Float16*)carve(n2a * dp * sizeof(_Float16));
+  float* r_n1 = (float*)carve(n2a * 4);
+  float* r_n2 = (float*)carve(n2a * 4);
   hipError_t e = hipMemcpy(d_probs, probs.data(), b_probs, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_d1, desc1, b_d1, hipMemcpyHostToDevice);
   if (e == hipSuccess && n2) e = hipMemcpy(d_d2, desc2, (size_t)n2 * dim * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = picp_launch_match_prep(nullptr, d_d1, n1, dim, q_h, q_n1, q_n2);
+  if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)
-    e = picp_launch_match(nullptr, n_problems, max_nq, d_d1, d_d2, d_probs, dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc);
+    e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
+                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc);
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);

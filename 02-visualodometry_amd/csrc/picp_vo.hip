@@ -206,6 +206,10 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
     a.map_xyz[3 * slot + 1] = o[1];
     a.map_xyz[3 * slot + 2] = o[2];
     for (int d = 0; d < dim; ++d) a.map_desc[slot * dim + d] = a.desc[(oc + pr.x) * dim + d];
+    // the matcher's prepped row of the same descriptor (fp16 + guard norms)
+    for (int d = 0; d < a.dp; ++d) a.map_h[slot * a.dp + d] = a.obs_h[(oc + pr.x) * a.dp + d];
+    a.map_n1[slot] = a.obs_n1[oc + pr.x];
+    a.map_n2[slot] = a.obs_n2[oc + pr.x];
   }
   if (threadIdx.x == 0) {
     const int64_t mn = s_base + cnt;

@@ -20,11 +20,16 @@
 #include "picp_host.h"
 #include "picp_internal.h"
 
-extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
-                                        const float* q_desc, const float* r_desc,
-                                        const MatchProblem* probs, int dim, float dist_thr,
-                                        float ratio_thr, int32_t* best_idx, float* best_dist,
-                                        float* second_dist, int32_t* accepted);
+extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* desc, int64_t n, int dim,
+                                             _Float16* h, float* n1, float* n2);
+extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
+                                             const float* q_desc, const float* r_desc,
+                                             const _Float16* q_h, const float* q_n1,
+                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
+                                             const MatchProblem* probs, int dim, float dist_thr,
+                                             float ratio_thr, int32_t* best_idx, float* best_dist,
+                                             float* second_dist, int32_t* accepted);
+extern "C" int picp_match_prep_kch(int dim);
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
@@ -52,6 +57,9 @@ struct picp_vo {
   float* desc_d = nullptr;
   int32_t *pm_bi = nullptr, *pm_acc = nullptr, *wm_bi = nullptr, *wm_acc = nullptr;
   float *pm_bd = nullptr, *pm_sd = nullptr, *wm_bd = nullptr, *wm_sd = nullptr;
+  int dp = 16;                     // matcher prep row width (halves)
+  _Float16* obs_h = nullptr;       // matcher prep of the observations
+  float *obs_n1 = nullptr, *obs_n2 = nullptr;
   // segments
   int n_seg = 0, max_steps = 0, npt = 1;
   int64_t map_slots = 0, n_slots = 0, cap_c = 0;
@@ -83,7 +91,7 @@ extern "C" int picp_vo_destroy(picp_vo_t* h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   vo_free_segments(h);
   void* bufs[] = {h->frame_off_d, h->uv_d, h->desc_d, h->pm_bi, h->pm_acc, h->wm_bi, h->wm_acc,
-                  h->pm_bd, h->pm_sd, h->wm_bd, h->wm_sd};
+                  h->pm_bd, h->pm_sd, h->wm_bd, h->wm_sd, h->obs_h, h->obs_n1, h->obs_n2};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
@@ -155,6 +163,10 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   VO_TRY(alloc((void**)&h->pm_sd, no * 4));
   VO_TRY(alloc((void**)&h->wm_bd, no * 4));
   VO_TRY(alloc((void**)&h->wm_sd, no * 4));
+  h->dp = 16 * picp_match_prep_kch(dim);
+  VO_TRY(alloc((void**)&h->obs_h, no * h->dp * sizeof(_Float16)));
+  VO_TRY(alloc((void**)&h->obs_n1, no * 4));
+  VO_TRY(alloc((void**)&h->obs_n2, no * 4));
   VO_TRY([&]() -> int {
     HIP_TRY(hipMemcpy(h->frame_off_d, frame_off, (size_t)(n_frames + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
     if (n_obs) {
@@ -162,6 +174,8 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
       HIP_TRY(hipMemcpy(h->desc_d, desc, (size_t)n_obs * dim * sizeof(float), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMemset(h->wm_acc, 0, no * 4));
+    HIP_TRY(picp_launch_match_prep(nullptr, h->desc_d, n_obs, dim, h->obs_h, h->obs_n1, h->obs_n2));
+    HIP_TRY(hipDeviceSynchronize());
     return PICP_OK;
   }());
 #undef VO_TRY
@@ -230,6 +244,9 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_poses = part((size_t)n_slots * 16 * sizeof(float));
   const Part p_steps = part((size_t)n_slots * sizeof(VoStep));
   const Part p_pairs = part((size_t)n_seg * cap_c * sizeof(int2));
+  const Part p_mh = part((size_t)map_slots * h->dp * sizeof(_Float16));
+  const Part p_mn1 = part((size_t)map_slots * sizeof(float));
+  const Part p_mn2 = part((size_t)map_slots * sizeof(float));
   HIP_TRY(hipMalloc(&h->seg_mem, total));
   char* m = (char*)h->seg_mem;
   h->segs = segs;
@@ -293,6 +310,13 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   V.poses = (float*)(m + p_poses.off);
   V.steps = (VoStep*)(m + p_steps.off);
   V.pairs = (int2*)(m + p_pairs.off);
+  V.dp = h->dp;
+  V.obs_h = h->obs_h;
+  V.obs_n1 = h->obs_n1;
+  V.obs_n2 = h->obs_n2;
+  V.map_h = (_Float16*)(m + p_mh.off);
+  V.map_n1 = (float*)(m + p_mn1.off);
+  V.map_n2 = (float*)(m + p_mn2.off);
   h->wprobs_d = V.wprobs;
   h->pprobs_d = (MatchProblem*)(m + p_pprobs.off);
   return PICP_OK;
@@ -303,14 +327,16 @@ static hipError_t vo_enqueue(picp_vo* h) {
   hipError_t e = hipSuccess;
   for (size_t p0 = 0; p0 < h->pprobs.size() && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
     const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, h->pprobs.size() - p0);
-    e = picp_launch_match(h->stream, np, h->max_obs, h->desc_d, h->desc_d, h->pprobs_d + p0, h->dim,
-                          VO_MATCH_DIST, VO_MATCH_RATIO, h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc);
+    e = picp_launch_match_mfma(h->stream, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1,
+                               h->obs_h, h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST,
+                               VO_MATCH_RATIO, h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc);
   }
   if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const VoArgs& V = h->vargs;
   for (int t = 0; t < h->max_steps && e == hipSuccess; ++t) {
-    e = picp_launch_match(h->stream, h->n_seg, h->max_obs, h->desc_d, V.map_desc, h->wprobs_d, h->dim,
-                          VO_MATCH_DIST, VO_MATCH_RATIO, h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc);
+    e = picp_launch_match_mfma(h->stream, h->n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
+                               V.map_h, V.map_n1, V.map_n2, h->wprobs_d, h->dim, VO_MATCH_DIST,
+                               VO_MATCH_RATIO, h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc);
     if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
     if (e == hipSuccess)
       e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,

@@ -7,6 +7,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["mfma", "exact"], autouse=True)
+def matcher_kernel(request, monkeypatch):
+    """Every test runs on both kernels: the MFMA pre-filter (default) and the exact scan
+    (PICP_MATCH_EXACT=1, read at each launch).  Both must give the oracle's bits."""
+    if request.param == "exact":
+        monkeypatch.setenv("PICP_MATCH_EXACT", "1")
+    else:
+        monkeypatch.delenv("PICP_MATCH_EXACT", raising=False)
+    return request.param
+
+
 def _eq(got, ref):
     for k in ("best_idx", "best_dist", "second_dist", "accepted"):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
@@ -64,3 +75,26 @@ def test_match_empty_and_errors(native):
     assert len(native.match_points(np.zeros((0, 10), np.float32), d)["best_idx"]) == 0
     with pytest.raises(Exception):
         native.match_points(np.ones((4, 33), np.float32), np.ones((4, 33), np.float32))
+
+
+def test_match_adversarial_fallbacks(native, oracle):
+    """The pre-filter's exits: exact duplicate references (ties, 0/0 ratio), a crowd of
+    references inside one query's candidate window (more than 16 candidates -> full scan),
+    components beyond fp16 range and non-finite ones (forced candidates / full scan)."""
+    rng = np.random.default_rng(5)
+    d2 = rng.uniform(-1, 1, (700, 10)).astype(np.float32)
+    d2[10] = d2[11] = d2[500]                      # triple duplicate
+    d2[600:660] = d2[600] + rng.normal(0, 1e-4, (60, 10)).astype(np.float32)  # 60 near-twins
+    d2[50, 3] = 1e6                                # beyond fp16 range
+    d2[51, 0] = np.nan
+    d2[52, 9] = np.inf
+    d1 = np.concatenate([d2[[10, 600, 601, 3, 50]] + 0.0, rng.uniform(-1, 1, (300, 10)).astype(np.float32)])
+    d1[5, 2] = 7e4                                 # query beyond fp16 range
+    d1[6, 1] = np.nan
+    _eq(native.match_points(d1, d2), oracle.match_points(d1, d2))
+    # large magnitudes everywhere (norms ~1e8): the bound scales with them
+    big = (rng.uniform(-1, 1, (400, 10)) * 3e3).astype(np.float32)
+    _eq(native.match_points(big[:150], big[150:], 1e9, 0.8), oracle.match_points(big[:150], big[150:], 1e9, 0.8))
+    # tiny magnitudes (fp16 subnormals)
+    tiny = (rng.uniform(-1, 1, (400, 10)) * 1e-5).astype(np.float32)
+    _eq(native.match_points(tiny[:150], tiny[150:], 1.0, 0.8), oracle.match_points(tiny[:150], tiny[150:], 1.0, 0.8))
