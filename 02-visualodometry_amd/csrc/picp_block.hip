@@ -14,13 +14,15 @@
 using namespace picp;
 
 #define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs
+#define PICP_BLDS_ITEMS 7680  // items staged in LDS: 5 x 4 B x 7680 = 150 KB of the 160 KB per CU
 
 template <int NPT, int PH>
 __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
-    PicpState* __restrict__ st_out) {
+    PicpState* __restrict__ st_out, int lds_items) {
+  extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   __shared__ float s_wave[PICP_BBLOCK / 64][PICP_NPART];
   __shared__ double s_tot[PICP_NPART];
   __shared__ float s_pose[12];
@@ -50,6 +52,23 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     zs[k] = Z[base + ic];
     us[k] = U[base + ic];
     vs[k] = V[base + ic];
+  }
+
+  // items NPT*BLOCK .. NPT*BLOCK + n_lds - 1 are staged in LDS once (read every round at LDS
+  // latency); any beyond that are streamed from L2/MALL every round
+  const int r0 = NPT * PICP_BBLOCK;
+  const int n_lds = max(0, min(n - r0, lds_items));
+  float* lx = s_lds;
+  float* ly = s_lds + lds_items;
+  float* lz = s_lds + 2 * lds_items;
+  float* lu = s_lds + 3 * lds_items;
+  float* lv = s_lds + 4 * lds_items;
+  for (int i = tid; i < n_lds; i += PICP_BBLOCK) {
+    lx[i] = X[base + r0 + i];
+    ly[i] = Y[base + r0 + i];
+    lz[i] = Z[base + r0 + i];
+    lu[i] = U[base + r0 + i];
+    lv[i] = V[base + r0 + i];
   }
 
   if (tid == 0) {  // initial state (as launch 0 of the multi-launch path)
@@ -95,7 +114,12 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
                       (f2){zs[k], zs[k1]}, (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]},
                       tid + k * PICP_BBLOCK < n, k + 1 < NPT && tid + (k + 1) * PICP_BBLOCK < n, a);
     }
-    for (int i = NPT * PICP_BBLOCK + tid; i < n; i += 2 * PICP_BBLOCK) {  // streamed remainder
+    for (int i = tid; i < n_lds; i += 2 * PICP_BBLOCK) {  // LDS-staged items, in pairs
+      const int i2 = min(i + PICP_BBLOCK, n_lds - 1);
+      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){lx[i], lx[i2]}, (f2){ly[i], ly[i2]}, (f2){lz[i], lz[i2]},
+                      (f2){lu[i], lu[i2]}, (f2){lv[i], lv[i2]}, true, i + PICP_BBLOCK < n_lds, a);
+    }
+    for (int i = r0 + n_lds + tid; i < n; i += 2 * PICP_BBLOCK) {  // streamed remainder
       const int i2 = min(i + PICP_BBLOCK, n - 1);
       const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
       const float x1 = X[base + i2], y1 = Y[base + i2], z1 = Z[base + i2], u1 = U[base + i2], v1 = V[base + i2];
@@ -134,20 +158,30 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part
 
+// max_n: the largest problem of the launch (sizes the LDS stage: max_n - npt*512 items, capped)
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
-                                        PicpState* st_out) {
+                                        PicpState* st_out, int max_n) {
   if (grid <= 0 || !args) return hipErrorInvalidValue;
   const bool ph = picp_use_pinhole(args->K);
-#define PICP_LAUNCH_B(N)                                                                                \
-  if (ph)                                                                                               \
-    hipLaunchKernelGGL((picp_block_kernel<N, 1>), dim3(grid), dim3(PICP_BBLOCK), 0, stream, X, Y, Z, U, \
-                       V, *args, probs, st_in, st_out);                                                \
-  else                                                                                                  \
-    hipLaunchKernelGGL((picp_block_kernel<N, 0>), dim3(grid), dim3(PICP_BBLOCK), 0, stream, X, Y, Z, U, \
-                       V, *args, probs, st_in, st_out)
+  const int lds_items = (max_n > npt * PICP_BBLOCK) ? min(max_n - npt * PICP_BBLOCK, PICP_BLDS_ITEMS) : 0;
+  const size_t lds_bytes = (size_t)5 * lds_items * sizeof(float);
+#define PICP_LAUNCH_B(N)                                                                                  \
+  if (ph) {                                                                                               \
+    if (lds_bytes > 65536)                                                                                \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                          (int)lds_bytes);                                                                \
+    hipLaunchKernelGGL((picp_block_kernel<N, 1>), dim3(grid), dim3(PICP_BBLOCK), lds_bytes, stream, X, Y, \
+                       Z, U, V, *args, probs, st_in, st_out, lds_items);                                  \
+  } else {                                                                                                \
+    if (lds_bytes > 65536)                                                                                \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                          (int)lds_bytes);                                                                \
+    hipLaunchKernelGGL((picp_block_kernel<N, 0>), dim3(grid), dim3(PICP_BBLOCK), lds_bytes, stream, X, Y, \
+                       Z, U, V, *args, probs, st_in, st_out, lds_items);                                  \
+  }
   switch (npt) {
     case 1: PICP_LAUNCH_B(1); break;
     case 2: PICP_LAUNCH_B(2); break;

@@ -63,6 +63,22 @@ __device__ __forceinline__ void acc2_fold(const Acc2& a, float v[PICP_NPART]) {
   v[31] = 0.0f;
 }
 
+// Correctly rounded 1/x in 3 instructions: v_rcp_f32 (about 1 ulp) and one FMA Newton step.
+// Verified bit-identical to the IEEE division 1.0f/x for EVERY float x in [2^-8, 2^8) by
+// picp_selftest_rcp (tests/test_gpu_parity.py); both operations are exact under power-of-two
+// scaling inside the normal range, so that covers every x with 2^-100 <= |x| <= 2^100
+// (rcp_safe).  Outside it (and for 0, inf, NaN) callers use the IEEE division.
+__device__ __forceinline__ float rcp_rn(float x) {
+  const float r = __builtin_amdgcn_rcpf(x);
+  const float e = fmaf(-x, r, 1.0f);
+  return fmaf(e, r, r);
+}
+
+__device__ __forceinline__ bool rcp_safe(float x) {
+  const float a = fabsf(x);
+  return (a >= 7.8886091e-31f) & (a <= 1.2676506e30f);  // [2^-100, 2^100]; NaN -> false
+}
+
 // ---------------------------------------------------------------------------------------
 // Per-correspondence math.  The block that decides projectability and the chi2 gate is
 // compiled with FP contraction OFF and evaluates every sum left to right, exactly like the
@@ -91,16 +107,16 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
     const float ix = ph0 * iz;
     const float iy = ph1 * iz;
     // src/camera.h:27-28 (z<=0 rejects; NaN passes as in the reference) and :31-34
-    valid = in_range && !(pc2 <= 0.0f) &&
-            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    // bitwise, not short-circuit: the same predicate without per-item exec-mask branches
+    valid = in_range & !(pc2 <= 0.0f) & !((ix < 0.0f) | (ix > C.maxx) | (iy < 0.0f) | (iy > C.maxy));
     e0 = ix - u;  // src/picp_solver.cpp:34
     e1 = iy - v;
     chi = e0 * e0 + e1 * e1;  // src/picp_solver.cpp:74
   }
   // src/picp_solver.cpp:75-89: strict gate, sqrt kernel weight, outliers only with keep
   const bool outlier = chi > thr;
-  const bool inl = valid && !outlier;
-  const bool use = inl || (valid && keep);
+  const bool inl = valid & !outlier;
+  const bool use = inl | (valid & keep);
   const float lambda = outlier ? sqrtf(thr / chi) : 1.0f;
   const float w = inl ? 1.0f : lambda;
   a.chi_in += inl ? chi : 0.0f;
@@ -183,15 +199,15 @@ __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, 
     iz = 1.0f / pc2;                  // ph2 == pc2 exactly
     const float ix = ph0 * iz;
     const float iy = ph1 * iz;
-    valid = in_range && !(pc2 <= 0.0f) &&
-            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    // bitwise, not short-circuit: the same predicate without per-item exec-mask branches
+    valid = in_range & !(pc2 <= 0.0f) & !((ix < 0.0f) | (ix > C.maxx) | (iy < 0.0f) | (iy > C.maxy));
     e0 = ix - u;
     e1 = iy - v;
     chi = e0 * e0 + e1 * e1;
   }
   const bool outlier = chi > thr;
-  const bool inl = valid && !outlier;
-  const bool use = inl || (valid && keep);
+  const bool inl = valid & !outlier;
+  const bool use = inl | (valid & keep);
   const float lambda = __builtin_amdgcn_rsqf(chi * inv_thr);
   const float w = use ? (inl ? 1.0f : lambda) : 0.0f;
   a.chi_in += inl ? chi : 0.0f;
@@ -270,15 +286,15 @@ __device__ __forceinline__ void item_general(const Pose& T, const Cam& C, float 
     iz = 1.0f / ph2;
     const float ix = ph0 * iz;
     const float iy = ph1 * iz;
-    valid = in_range && !(pc2 <= 0.0f) &&
-            !(ix < 0.0f || ix > C.maxx || iy < 0.0f || iy > C.maxy);
+    // bitwise, not short-circuit: the same predicate without per-item exec-mask branches
+    valid = in_range & !(pc2 <= 0.0f) & !((ix < 0.0f) | (ix > C.maxx) | (iy < 0.0f) | (iy > C.maxy));
     e0 = ix - u;
     e1 = iy - v;
     chi = e0 * e0 + e1 * e1;
   }
   const bool outlier = chi > thr;
-  const bool inl = valid && !outlier;
-  const bool use = inl || (valid && keep);
+  const bool inl = valid & !outlier;
+  const bool use = inl | (valid & keep);
   const float lambda = outlier ? sqrtf(thr / chi) : 1.0f;
   o.w = use ? (inl ? 1.0f : lambda) : 0.0f;
   o.chi = chi;
@@ -342,7 +358,7 @@ __device__ __forceinline__ void acc2_normal(const f2 J0[6], const f2 J1[6], f2 e
 __device__ __forceinline__ void acc2_stats(f2 chi, bool inlA, bool inlB, bool validA, bool validB,
                                            Acc2& a) {
   a.chi_in += (f2){inlA ? chi.x : 0.0f, inlB ? chi.y : 0.0f};
-  a.chi_out += (f2){(validA && !inlA) ? chi.x : 0.0f, (validB && !inlB) ? chi.y : 0.0f};
+  a.chi_out += (f2){(validA & !inlA) ? chi.x : 0.0f, (validB & !inlB) ? chi.y : 0.0f};
   a.n_in += (f2){inlA ? 1.0f : 0.0f, inlB ? 1.0f : 0.0f};
   a.n_proj += (f2){validA ? 1.0f : 0.0f, validB ? 1.0f : 0.0f};
 }
@@ -363,21 +379,29 @@ __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C,
     pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
     ph0 = C.k00 * pc0 + C.k02 * pc2;  // src/camera.h:29 without the zero terms
     ph1 = C.k11 * pc1 + C.k12 * pc2;
-    iz.x = 1.0f / pc2.x;              // ph2 == pc2 exactly; correctly rounded per item
-    iz.y = 1.0f / pc2.y;
+    // ph2 == pc2 exactly; the correctly rounded reciprocal per item (rcp_rn, exhaustively
+    // verified), the IEEE division only when a lane of the wave holds an extreme value
+    if (__all(rcp_safe(pc2.x) & rcp_safe(pc2.y))) {
+      iz.x = rcp_rn(pc2.x);
+      iz.y = rcp_rn(pc2.y);
+    } else {
+      iz.x = 1.0f / pc2.x;
+      iz.y = 1.0f / pc2.y;
+    }
     const f2 ix = ph0 * iz;
     const f2 iy = ph1 * iz;
-    validA = inA && !(pc2.x <= 0.0f) &&
-             !(ix.x < 0.0f || ix.x > C.maxx || iy.x < 0.0f || iy.x > C.maxy);
-    validB = inB && !(pc2.y <= 0.0f) &&
-             !(ix.y < 0.0f || ix.y > C.maxx || iy.y < 0.0f || iy.y > C.maxy);
+    // bitwise, not short-circuit: the same predicate without per-item exec-mask branches
+    validA = inA & !(pc2.x <= 0.0f) &
+             !((ix.x < 0.0f) | (ix.x > C.maxx) | (iy.x < 0.0f) | (iy.x > C.maxy));
+    validB = inB & !(pc2.y <= 0.0f) &
+             !((ix.y < 0.0f) | (ix.y > C.maxx) | (iy.y < 0.0f) | (iy.y > C.maxy));
     e0 = ix - u;
     e1 = iy - v;
     chi = e0 * e0 + e1 * e1;
   }
   const bool outA = chi.x > thr, outB = chi.y > thr;
-  const bool inlA = validA && !outA, inlB = validB && !outB;
-  const bool useA = inlA || (validA && keep), useB = inlB || (validB && keep);
+  const bool inlA = validA & !outA, inlB = validB & !outB;
+  const bool useA = inlA | (validA & keep), useB = inlB | (validB & keep);
   const f2 q = chi * inv_thr;
   const f2 w = {useA ? (inlA ? 1.0f : __builtin_amdgcn_rsqf(q.x)) : 0.0f,
                 useB ? (inlB ? 1.0f : __builtin_amdgcn_rsqf(q.y)) : 0.0f};

@@ -372,3 +372,17 @@ extern "C" hipError_t picp_launch_triangulate(hipStream_t stream, const float* P
                      P1, P2, uv1, uv2, q, xyz);
   return hipGetLastError();
 }
+
+// ------------------------------- self-test of rcp_rn ----------------------------------
+// Counts the floats x = 2^e * (1 + k 2^-23), e in [e_lo, e_hi), k in [0, 2^23), of both signs
+// for which rcp_rn(x) and the IEEE division 1.0f / x differ in any bit.
+extern "C" __global__ void picp_rcp_check_kernel(int e_lo, int e_hi, unsigned long long* bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)1 << 24;  // 2^23 mantissas x 2 signs per binade
+  if (i >= (int64_t)(e_hi - e_lo) * per) return;
+  const int e = e_lo + (int)(i / per);
+  const unsigned rem = (unsigned)(i % per);
+  const unsigned bits = ((rem >> 23) << 31) | ((unsigned)(e + 127) << 23) | (rem & 0x7fffffu);
+  const float x = __uint_as_float(bits);
+  if (__float_as_uint(rcp_rn(x)) != __float_as_uint(1.0f / x)) atomicAdd(bad, 1ull);
+}

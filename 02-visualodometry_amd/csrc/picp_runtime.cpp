@@ -37,7 +37,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
-                                        PicpState* st_out);
+                                        PicpState* st_out, int max_n);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_persistent_block(void);
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
@@ -55,6 +55,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted);
 extern "C" int picp_match_prep_kch(int dim);
+extern "C" __global__ void picp_rcp_check_kernel(int e_lo, int e_hi, unsigned long long* bad);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -140,6 +141,7 @@ static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // batch
 // ------------------------------------------------------------------------------------
 struct picp_batch {
+  int64_t max_n = 0;           // largest problem (block mode sizes its LDS stage with it)
   int device = 0;
   hipStream_t stream = nullptr;
   int np = 0;
@@ -248,6 +250,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     const bool force_block = m && strcmp(m, "block") == 0;
     int64_t max_n = 0;
     for (int i = 0; i < np; ++i) max_n = std::max<int64_t>(max_n, offs[i + 1] - offs[i]);
+    b->max_n = max_n;
     int bnpt = 0;  // block mode: register-resident correspondences per lane (rest streamed)
     {
       int cap = picp_block_max_items() / 512;
@@ -444,7 +447,7 @@ static hipError_t graph_prologue(picp_batch* b) {
 static hipError_t enqueue_solve(picp_batch* b, int R) {
   if (b->mode == PICP_MODE_BLOCK)
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
-                             b->probs_d, b->init_d, b->st_d[0]);
+                             b->probs_d, b->init_d, b->st_d[0], (int)b->max_n);
   if (b->mode == PICP_MODE_PERSISTENT) {
     // every polled word (error word and all granules) is zeroed before each launch
     hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
@@ -1111,4 +1114,26 @@ extern "C" int picp_match(int device, const float* desc1, int64_t n1, const floa
   const int64_t o1[2] = {0, n1}, o2[2] = {0, n2};
   return picp_match_batch(device, 1, o1, o2, desc1, desc2, dim, dist_thr, ratio_thr, best_idx, best_dist,
                           second_dist, accepted);
+}
+
+// ------------------------------------------------------------------------------------
+// self-test: the fast correctly rounded reciprocal of the projection (picp_device.h rcp_rn)
+// ------------------------------------------------------------------------------------
+extern "C" int picp_selftest_rcp(int device, int e_lo, int e_hi, uint64_t* mismatches) {
+  CHECK_ARG(mismatches && e_lo >= -126 && e_hi <= 127 && e_lo < e_hi, "picp_selftest_rcp: bad argument");
+  HIP_TRY(hipSetDevice(device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, sizeof(unsigned long long));
+  const int64_t n = (int64_t)(e_hi - e_lo) << 24;
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(picp_rcp_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, e_lo, e_hi, d);
+    e = hipGetLastError();
+  }
+  unsigned long long h = 0;
+  if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_selftest_rcp: %s", hipGetErrorString(e));
+  *mismatches = h;
+  return PICP_OK;
 }

@@ -34,7 +34,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
-                                        PicpState* st_out);
+                                        PicpState* st_out, int max_n);
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
 
@@ -340,7 +340,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
     if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
     if (e == hipSuccess)
       e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,
-                            V.st_in, (PicpState*)V.st_out);
+                            V.st_in, (PicpState*)V.st_out, (int)h->max_obs);
     if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &V, t);
   }
   return e;

@@ -43,7 +43,7 @@ EXPORTED = [
     "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
     "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async",
     "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
-    "picp_vo_info",
+    "picp_vo_info", "picp_selftest_rcp",
 ]
 
 
@@ -139,6 +139,7 @@ def lib():
         "picp_vo_get_steps": ([vp, ctypes.POINTER(VOStep)], i),
         "picp_vo_get_map": ([vp, i, i64, fp, fp, ctypes.POINTER(i64)], i),
         "picp_vo_time": ([vp, i, fp], i),
+        "picp_selftest_rcp": ([i, i, i, ctypes.POINTER(ctypes.c_uint64)], i),
         "picp_vo_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i)], i),
     }
     for name, (args, res) in sig.items():
@@ -505,3 +506,11 @@ class VOSequence:
         desc = np.zeros(max(n.value, 1) * self.dim, np.float32)
         _check(lib().picp_vo_get_map(self._h, seg, n.value, _fptr(xyz), _fptr(desc), ctypes.byref(n)))
         return xyz[:3 * n.value].reshape(-1, 3), desc[:self.dim * n.value].reshape(-1, self.dim)
+
+
+def selftest_rcp(e_lo=-8, e_hi=8, device=0):
+    """Floats (both signs, exponents [e_lo, e_hi)) where the kernels' fast reciprocal differs
+    from the IEEE division; 0 proves it for every |x| in [2^-100, 2^100] (picp_device.h)."""
+    n = ctypes.c_uint64()
+    _check(lib().picp_selftest_rcp(device, e_lo, e_hi, ctypes.byref(n)))
+    return n.value

@@ -221,6 +221,13 @@ int picp_vo_get_map(picp_vo_t* h, int seg, int64_t cap, float* xyz, float* desc,
 int picp_vo_time(picp_vo_t* h, int reps, float* ms_per_run);
 int picp_vo_info(picp_vo_t* h, int64_t* n_obs, int64_t* n_slots, int64_t* map_slots, int* npt);
 
+/* ---------------- self-test ---------------- */
+/* The projection's reciprocal 1/z must be the correctly rounded one (src/camera.h:30; the
+ * chi2 gate is bit-exact): the kernels use a 3-instruction form, valid for every float in
+ * [2^-100, 2^100] iff it matches the IEEE division on every float of a binade range.  Counts
+ * the mismatching floats of both signs with exponents in [e_lo, e_hi); expected 0. */
+int picp_selftest_rcp(int device, int e_lo, int e_hi, uint64_t* mismatches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -416,3 +416,11 @@ def test_uniform_multi_frame_batch_modes(native, oracle, mode, P, n):
     # repeated replays of the same graph give identical results (granules re-zeroed per launch)
     b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
     np.testing.assert_array_equal(b.poses(), poses)
+
+
+def test_fast_reciprocal_is_correctly_rounded(native):
+    """The projection's 1/z (src/camera.h:30) feeds the bit-exact gate.  The kernels compute it
+    as v_rcp + one FMA Newton step; over the 16 binades [2^-8, 2^8), both signs (268M floats),
+    it must equal the IEEE division bit for bit -- which, by power-of-two scaling, proves it
+    for every |z| in [2^-100, 2^100] (outside: the kernels use the division)."""
+    assert native.selftest_rcp(-8, 8) == 0
