@@ -1,7 +1,7 @@
 // icp_test -- the reference's published pipeline (exec/icp_test.cpp:17-215) driven through the
 // drop-in pr:: facade, i.e. on the MI355X PICP + triangulation kernels.
 //
-//   icp_test [data_dir=./data] [out_dir=./output] [--fused] [--frames N] [--device D]
+//   icp_test [data_dir=./data] [out_dir=./output] [--fused | --vo] [--frames N] [--device D]
 //
 // Per frame, as the reference: match the next frame's descriptors to the map
 // (match_points, src/my_utilities.h:70-120), PICP from the previous pose (threshold 3000, <= 50
@@ -14,6 +14,9 @@
 // normalised to unit translation -- what cv::findEssentialMat + cv::recoverPose
 // (src/cam.cpp:37-91, OpenCV RANSAC, out of scope) return for noise-free matches.  --fused runs
 // the icp loop as one device solve (pr::PICPSolver::solve) instead of host-driven oneRound().
+// Descriptor matching runs on the GPU matcher (picp_match).  --vo runs the whole per-frame loop
+// device-resident (picp_vo_*: match, PICP, match, select, triangulate, append on the GPU) and
+// then writes the same outputs.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -87,34 +90,27 @@ bool read_measurement(const std::string& path, Measurement& m) {
   return true;
 }
 
-float desc_dist2(const float* a, const float* b) {
-  float s = 0.f;
-  for (int k = 0; k < kDesc; ++k) {
-    const float d = a[k] - b[k];
-    s += d * d;
-  }
-  return s;
-}
+int g_device = 0;
 
-// src/my_utilities.h:70-120: nearest descriptor, absolute threshold and Lowe ratio.
+// src/my_utilities.h:70-120 on the GPU matcher (picp_match): nearest descriptor, absolute
+// threshold and Lowe ratio, bit-identical to the reference's scan.
 // corr.first = index in set 1, corr.second = index in set 2.
 template <class A, class B>
 void match_points(const std::vector<A>& p1, const std::vector<B>& p2, pr::IntPairVector& corr) {
-  for (size_t i = 0; i < p1.size(); ++i) {
-    float best = std::numeric_limits<float>::max(), second = best;
-    int bi = -1;
-    for (size_t j = 0; j < p2.size(); ++j) {
-      const float d = desc_dist2(p1[i].desc, p2[j].desc);
-      if (d < best) {
-        second = best;
-        best = d;
-        bi = (int)j;
-      } else if (d < second) {
-        second = d;
-      }
-    }
-    if (bi != -1 && best < kDistanceThreshold && best / second < kRatioThreshold) corr.emplace_back((int)i, bi);
+  if (p1.empty()) return;
+  std::vector<float> d1(p1.size() * kDesc), d2(std::max<size_t>(p2.size(), 1) * kDesc);
+  for (size_t i = 0; i < p1.size(); ++i) std::memcpy(&d1[i * kDesc], p1[i].desc, sizeof(p1[i].desc));
+  for (size_t j = 0; j < p2.size(); ++j) std::memcpy(&d2[j * kDesc], p2[j].desc, sizeof(p2[j].desc));
+  std::vector<int32_t> bi(p1.size()), acc(p1.size());
+  std::vector<float> best(p1.size()), second(p1.size());
+  if (picp_match(g_device, d1.data(), (int64_t)p1.size(), d2.data(), (int64_t)p2.size(), kDesc,
+                 kDistanceThreshold, kRatioThreshold, bi.data(), best.data(), second.data(),
+                 acc.data()) != PICP_OK) {
+    std::cerr << "match_points failed: " << picp_last_error() << std::endl;
+    std::exit(EXIT_FAILURE);
   }
+  for (size_t i = 0; i < p1.size(); ++i)
+    if (acc[i]) corr.emplace_back((int)i, bi[i]);
 }
 
 pr::Isometry3f planar_pose(const float p[3]) {  // augment_pose, src/my_utilities.cpp:245-260
@@ -209,16 +205,18 @@ double umeyama_scale(const std::vector<pr::Vector3f>& P, const std::vector<pr::V
 
 int main(int argc, char** argv) {
   std::string data_dir = "./data", out_dir = "./output";
-  bool fused = false;
+  bool fused = false, vo = false;
   int n_meas = 121, device = 0, pos = 0;
   for (int a = 1; a < argc; ++a) {
     std::string s = argv[a];
     if (s == "--fused") fused = true;
+    else if (s == "--vo") vo = true;
     else if (s == "--frames" && a + 1 < argc) n_meas = std::atoi(argv[++a]);
     else if (s == "--device" && a + 1 < argc) device = std::atoi(argv[++a]);
     else if (pos == 0) { data_dir = s; ++pos; }
     else if (pos == 1) { out_dir = s; ++pos; }
   }
+  g_device = device;
   std::vector<Measurement> meas(n_meas);
   for (int i = 0; i < n_meas; ++i) {
     char name[64];
@@ -266,10 +264,74 @@ int main(int argc, char** argv) {
   pr::Vector3f t01 = T01.translation();
   const float tn = t01.norm();
   T01(0, 3) = t01[0] / tn; T01(1, 3) = t01[1] / tn; T01(2, 3) = t01[2] / tn;
-  triangulate(pr::Isometry3f::Identity(), T01, meas[0].points, meas[1].points, init_corr);
-
   long total_rounds = 0;
   double picp_ms = 0;
+  if (vo) {
+    // the whole loop below, device-resident: one VO segment over frames 0 .. n_meas-1 with the
+    // bootstrap pair (Identity, T01) (picp_vo_*, include/picp_c.h)
+    std::vector<int64_t> off(n_meas + 1, 0);
+    for (int f = 0; f < n_meas; ++f) off[f + 1] = off[f] + (int64_t)meas[f].points.size();
+    std::vector<float> uv((size_t)off[n_meas] * 2), desc((size_t)off[n_meas] * kDesc);
+    for (int f = 0; f < n_meas; ++f)
+      for (size_t i = 0; i < meas[f].points.size(); ++i) {
+        const DataPoint& d = meas[f].points[i];
+        uv[2 * (off[f] + i)] = d.u;
+        uv[2 * (off[f] + i) + 1] = d.v;
+        std::memcpy(&desc[(off[f] + i) * kDesc], d.desc, sizeof(d.desc));
+      }
+    picp_vo_t* seq = nullptr;
+    if (picp_vo_create(&seq, device, 480, 640, pr::data9(K), n_meas, off.data(), uv.data(), desc.data(),
+                       kDesc) != PICP_OK) {
+      std::cerr << "picp_vo_create failed: " << picp_last_error() << std::endl;
+      return EXIT_FAILURE;
+    }
+    float boot[32];
+    std::memcpy(boot, pr::data16(pr::Isometry3f::Identity()), 16 * sizeof(float));
+    std::memcpy(boot + 16, pr::data16(T01), 16 * sizeof(float));
+    picp_params prm;
+    picp_params_default(&prm);
+    prm.threshold = 3000.0f;
+    const int64_t first = 0;
+    const int32_t steps = n_meas - 1;
+    auto t0 = std::chrono::steady_clock::now();
+    if (picp_vo_set_segments(seq, 1, &first, &steps, boot, &prm) != PICP_OK || picp_vo_run(seq) != PICP_OK) {
+      std::cerr << "picp_vo run failed: " << picp_last_error() << std::endl;
+      return EXIT_FAILURE;
+    }
+    picp_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<float> P16((size_t)n_meas * 16);
+    std::vector<picp_vo_step> rec(n_meas);
+    int64_t mn = 0;
+    if (picp_vo_get_poses(seq, P16.data()) != PICP_OK || picp_vo_get_steps(seq, rec.data()) != PICP_OK ||
+        picp_vo_get_map(seq, 0, 0, nullptr, nullptr, &mn) != PICP_OK) {
+      std::cerr << "picp_vo readback failed: " << picp_last_error() << std::endl;
+      return EXIT_FAILURE;
+    }
+    std::vector<float> mxyz((size_t)std::max<int64_t>(mn, 1) * 3), mdesc((size_t)std::max<int64_t>(mn, 1) * kDesc);
+    picp_vo_get_map(seq, 0, mn, mxyz.data(), mdesc.data(), &mn);
+    picp_vo_destroy(seq);
+    poses.clear();
+    for (int f = 0; f < n_meas; ++f) {
+      poses.push_back(pr::iso_from16(&P16[(size_t)f * 16]));
+      gt_poses.push_back(planar_pose(meas[f].gt));
+      total_rounds += f ? rec[f].rounds : 0;
+    }
+    // a map point carries the descriptor (and so the ids) of the observation it came from
+    for (int64_t k = 0; k < mn; ++k) {
+      WorldPoint w;
+      std::memcpy(w.xyz, &mxyz[k * 3], sizeof(w.xyz));
+      std::memcpy(w.desc, &mdesc[k * kDesc], sizeof(w.desc));
+      for (int f = 0; f < n_meas && w.id_real < 0; ++f)
+        for (auto& d : meas[f].points)
+          if (std::memcmp(d.desc, w.desc, sizeof(w.desc)) == 0) {
+            w.id_meas = d.id_meas;
+            w.id_real = d.id_real;
+            break;
+          }
+      world.push_back(w);
+    }
+  } else {
+  triangulate(pr::Isometry3f::Identity(), T01, meas[0].points, meas[1].points, init_corr);
   for (int i = 0; i < n_meas - 1; i++) {
     gt_poses.push_back(planar_pose(meas[i].gt));
     const std::vector<DataPoint>& curr = meas[i].points;
@@ -318,6 +380,7 @@ int main(int argc, char** argv) {
     triangulate(previous_pose, estimated_pose, curr, next, to_tri);
   }
   gt_poses.push_back(planar_pose(meas[n_meas - 1].gt));
+  }
 
   const pr::Isometry3f C2I = camera_to_image();
   std::vector<pr::Vector3f> P, Q;
@@ -363,8 +426,8 @@ int main(int argc, char** argv) {
   const double n = (double)poses.size();
   std::printf("{\"frames\": %d, \"world_points\": %zu, \"scale\": %.6f, \"trans_err_mean\": %.6f, "
               "\"trans_err_rmse\": %.6f, \"trans_err_max\": %.6f, \"yaw_err_wrapped_mean\": %.6f, "
-              "\"yaw_err_wrapped_max\": %.6f, \"picp_rounds\": %ld, \"picp_ms\": %.3f, \"fused\": %d}\n",
+              "\"yaw_err_wrapped_max\": %.6f, \"picp_rounds\": %ld, \"picp_ms\": %.3f, \"fused\": %d, \"vo\": %d}\n",
               (int)n, world.size(), scale, sum_e / n, std::sqrt(sum_e2 / n), max_e, sum_yaw / n, max_yaw,
-              total_rounds, picp_ms, fused ? 1 : 0);
+              total_rounds, picp_ms, fused ? 1 : 0, vo ? 1 : 0);
   return 0;
 }

@@ -60,3 +60,21 @@ def test_icp_test_pipeline_on_reference_data(vo, tmp_path):
     assert 200 <= s_host["world_points"] <= 5000
     # unit-baseline bootstrap: frame steps ~1 in VO units, scale ~0.2 m per unit
     assert 0.1 < s_host["scale"] < 0.4
+
+
+@pytest.mark.gpu
+def test_icp_test_device_resident_vo_mode(vo, tmp_path):
+    """--vo: the same pipeline with the per-frame loop device-resident (picp_vo_*).  The map is
+    built by descriptor matching alone, so it holds the same landmarks as the host-driven loop
+    (and the reference's published 490); the trajectory agrees within the chaotic band of the
+    free-running sequence (tests/test_gpu_vo.py)."""
+    s_host, e_host, t_host = _run(tmp_path, vo)
+    s_vo, e_vo, t_vo = _run(tmp_path, vo, "--vo")
+    assert s_vo["vo"] == 1 and s_vo["frames"] == 121
+    assert s_vo["world_points"] == s_host["world_points"]
+    ids_host = np.loadtxt(tmp_path / "out" / "estimated_world_points.txt")[:, 0]
+    ids_vo = np.loadtxt(tmp_path / "out--vo" / "estimated_world_points.txt")[:, 0]
+    np.testing.assert_array_equal(np.sort(ids_host), np.sort(ids_vo))
+    assert set(ids_vo.astype(int).tolist()) == set(vo.ref_map_ids.tolist())
+    np.testing.assert_allclose(t_host[:, 1:3], t_vo[:, 1:3], atol=2e-2)
+    assert s_vo["trans_err_max"] < 2 * float(vo.ref_errors[:, 1].max())
