@@ -10,5 +10,5 @@ tail -1 gpurun_out/pmc/${WL}_trace.log
 cat gpurun_out/pmc/${WL}_trace/run_kernel_stats.csv
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C -d gpurun_out/pmc/${WL}_$C -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/${WL}_$C.log 2>&1 || { echo pmc $C failed; tail gpurun_out/pmc/${WL}_$C.log; exit 1; }
-  python3 tools/parse_pmc.py gpurun_out/pmc/${WL}_$C/run_counter_collection.csv picp_round_kernel
+  python3 tools/parse_pmc.py gpurun_out/pmc/${WL}_$C/run_counter_collection.csv ${KERNEL:-picp_}
 done

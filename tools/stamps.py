@@ -2,8 +2,8 @@
 """Phase breakdown of picp_round_kernel from the diagnostic stamp build (GPU).
 
 Stamps (s_memrealtime, 10 ns ticks), thread 0 of each block, launches j=10 and j=11:
-  0 kernel entry, 1 problem/state fetched, 2 partials reduced, 3 solve done (barrier),
-  4 linearize loop done, 5 partial written.
+  0 kernel entry, 1 state read, 2 linearize loop done, 3 partial published + ticket taken,
+  4 (last arriver only) all partials reduced, 5 (last arriver only) round finished.
 """
 import argparse
 import ctypes
@@ -44,14 +44,18 @@ def main():
         st = buf[jj, :nb].astype(np.int64)
         t0 = st[:, 0].min()
         rel = (st - t0) * 10  # ns
-        names = ["entry", "issued", "reduced", "solved", "linearized", "written", "tid0_solve_end"]
-        print("launch j=%d, %d blocks (ns from first block entry): median / max per stamp" % (10 + jj, nb))
-        for k, nm in [(k, nm) for k, nm in enumerate(names) if k != 6] + [(6, names[6])]:
+        print("launch j=%d, %d blocks (ns from the first block's entry)" % (10 + jj, nb))
+        for k, nm in enumerate(["entry", "state", "linearized", "published"]):
             print("  %-10s median %7d  max %7d" % (nm, np.median(rel[:, k]), rel[:, k].max()))
-        d = np.diff(rel[:, :6], axis=1)
-        print("  phase durations median:", dict(zip(["fetch", "reduce", "solve", "linearize", "write"], np.median(d, 0).astype(int).tolist())))
+        last = np.nonzero(st[:, 4] > st[:, 3])[0]  # the last arriver stamped 4 and 5 this launch
+        if len(last):
+            i = last[np.argmax(st[last, 4])]
+            print("  last arriver (block %d): reduced %d, finished %d  (reduce %d ns, solve %d ns)"
+                  % (i, rel[i, 4], rel[i, 5], rel[i, 4] - rel[i, 3], rel[i, 5] - rel[i, 4]))
+        d = np.diff(rel[:, :4], axis=1)
+        print("  phase medians:", dict(zip(["state", "linearize", "publish"], np.median(d, 0).astype(int).tolist())))
     gap = (buf[1, :nb, 0].astype(np.int64).min() - buf[0, :nb, 5].astype(np.int64).max()) * 10
-    print("gap last block end (j=10) -> first block entry (j=11): %d ns" % gap)
+    print("gap round end (j=10) -> first block entry (j=11): %d ns" % gap)
 
 
 if __name__ == "__main__":
