@@ -176,12 +176,16 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   // beyond the 2 resident waves per SIMD).  Single frames (VEC = 1) are latency-bound: one slot.
   constexpr int RING = (VEC == 4) ? 3 : 1;
   float bx[RING][NI], by[RING][NI], bz[RING][NI], bu[RING][NI], bv[RING][NI];
-  // The first steps do not depend on the pose, so their latency overlaps the state read below.
+  // The state (the pose) is loaded FIRST: loads return in order, so a state load issued behind
+  // the ring's 15 prefetches would wait for all of them (stamps: ~4.5 us at 16M).  The first
+  // steps do not depend on the pose, so their latency overlaps the state's.
+  int32_t st_word = 0;
+  if (tid < 32) st_word = reinterpret_cast<const int32_t*>(st_in + p)[tid];
 #pragma unroll
   for (int sl = 0; sl < RING; ++sl)
     if (c0 + sl * STEP < count) load_step(c0 + sl * STEP, bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
 
-  if (tid < 32) s_state[tid] = reinterpret_cast<const int32_t*>(st_in + p)[tid];
+  if (tid < 32) s_state[tid] = st_word;
   __syncthreads();
   if (j == 0 && tid == 0) {  // the icp_test loop state at entry (exec/icp_test.cpp:89)
     PicpState& s = *reinterpret_cast<PicpState*>(s_state);

@@ -204,7 +204,7 @@ static void drop_graph(picp_batch* b) {
   b->g_rounds = -1;
 }
 
-static int items_per_block(int64_t total) {
+static int items_per_block(int64_t total, int num_cu) {
   const char* env = getenv("PICP_ITEMS_PER_BLOCK");
   if (env) {
     int v = atoi(env);
@@ -216,9 +216,17 @@ static int items_per_block(int64_t total) {
   if (total <= ((int64_t)1 << 18)) return 2 * PICP_BLOCK;  // measured best for C2 (tools/sweep.py)
   // streaming: about two resident 256-thread blocks per CU (all blocks in flight at once),
   // each streaming its slice through the prefetch ring (profiles/r01/sweep_*m_*.log)
-  if (total >= (int64_t)8 << 20) return PICP_BLOCK * 4 * 32;
-  if (total >= (int64_t)2 << 20) return PICP_BLOCK * 4 * 8;
-  return PICP_BLOCK * 4 * 2;
+  if (total < (int64_t)2 << 20) return PICP_BLOCK * 4 * 2;
+  if (total < (int64_t)8 << 20) return PICP_BLOCK * 4 * 8;
+  // Round the block count to a multiple of 2 x CUs so every CU carries the same load: with 489
+  // blocks on 256 CUs some CUs hold one block and some two, and the round waits for the slowest
+  // (16M: 489 blocks 69.0 us/round, 512 blocks 66.5 us; at 2M/4M the difference is in the noise;
+  // profiles/r01/sweep_balance.log).
+  const int64_t target = PICP_BLOCK * 4 * 32;
+  const int64_t unit = 2 * (int64_t)std::max(1, num_cu);
+  int64_t nb = ((total + target - 1) / target + unit / 2) / unit * unit;
+  nb = std::max(nb, unit);
+  return (int)round_up((total + nb - 1) / nb, 4);
 }
 
 // (Re)build the partition for correspondence offsets `offs` (np+1 entries).
@@ -241,7 +249,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
   //                  block of the batch is resident at once (uniform problems);
   //  * GRAPH      -- one launch per round, replayed from a hipGraph: everything else.
   // PICP_MODE=graph|persistent|block forces a mode when the batch is eligible for it.
-  int ipb = items_per_block(b->total);
+  int ipb = items_per_block(b->total, b->num_cu);
   b->mode = PICP_MODE_GRAPH;
   {
     const char* m = getenv("PICP_MODE");
