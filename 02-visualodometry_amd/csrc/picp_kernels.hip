@@ -19,6 +19,7 @@
 
 #include <float.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "picp_internal.h"
 
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const int4* __restrict__ blkinfo,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
-    unsigned long long* __restrict__ part, unsigned int* __restrict__ tickets, int j) {
+    unsigned long long* __restrict__ part, unsigned int* __restrict__ tickets, int j, int rev_sweep) {
   __shared__ double s_red[16][PICP_NPART + 1];
   __shared__ double s_tot[PICP_NPART];
   __shared__ float s_wave[PICP_BLOCK / 64][PICP_NPART];
@@ -176,6 +177,13 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   // beyond the 2 resident waves per SIMD).  Single frames (VEC = 1) are latency-bound: one slot.
   constexpr int RING = (VEC == 4) ? 3 : 1;
   float bx[RING][NI], by[RING][NI], bz[RING][NI], bu[RING][NI], bv[RING][NI];
+  // Odd rounds sweep the slice backwards (VEC = 4: float4 position c -> cnt4 - 4 - c, still one
+  // contiguous run per wave): a round then starts on the lines the previous round touched last,
+  // which the 256 MiB Infinity Cache still holds when the planes outgrow it (16M: 305 MiB).  The
+  // per-lane summation order is fixed by (j, rev_sweep), so replays are deterministic.
+  const int cnt4 = (count + 3) & ~3;
+  const bool rev = (VEC == 4) && rev_sweep;
+  auto phys = [&](int c) { return rev ? cnt4 - 4 - c : c; };
   // The state (the pose) is loaded FIRST: loads return in order, so a state load issued behind
   // the ring's 15 prefetches would wait for all of them (stamps: ~4.5 us at 16M).  The first
   // steps do not depend on the pose, so their latency overlaps the state's.
@@ -183,7 +191,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   if (tid < 32) st_word = reinterpret_cast<const int32_t*>(st_in + p)[tid];
 #pragma unroll
   for (int sl = 0; sl < RING; ++sl)
-    if (c0 + sl * STEP < count) load_step(c0 + sl * STEP, bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
+    if (c0 + sl * STEP < count) load_step(phys(c0 + sl * STEP), bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
 
   if (tid < 32) s_state[tid] = st_word;
   __syncthreads();
@@ -228,14 +236,15 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
     for (int sl = 0; sl < RING; ++sl) {
       const int cs = c + sl * STEP;
       if (cs < count) {
+        const int ps = phys(cs);
 #pragma unroll
         for (int k = 0; k < NI; k += 2)
           accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){bx[sl][k], bx[sl][k + 1]},
                           (f2){by[sl][k], by[sl][k + 1]}, (f2){bz[sl][k], bz[sl][k + 1]},
                           (f2){bu[sl][k], bu[sl][k + 1]}, (f2){bv[sl][k], bv[sl][k + 1]},
-                          cs + k * ISTRIDE < count, cs + (k + 1) * ISTRIDE < count, a);
+                          ps + k * ISTRIDE < count, ps + (k + 1) * ISTRIDE < count, a);
         const int cn = cs + RING * STEP;
-        if (cn < count) load_step(cn, bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
+        if (cn < count) load_step(phys(cn), bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
       }
     }
   }
@@ -339,10 +348,14 @@ extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, c
                                         const PicpState* st_in, PicpState* st_out,
                                         unsigned long long* part, unsigned int* tickets, int j) {
   if (grid <= 0 || !args || !part || !tickets) return hipErrorInvalidValue;
+  // odd rounds sweep backwards (Infinity-Cache reuse); PICP_SWEEP_FORWARD=1 disables (A/B)
+  const char* fwd = getenv("PICP_SWEEP_FORWARD");  // read per launch: graphs capture it
+  const bool forward_only = fwd && atoi(fwd) != 0;
+  const int rev = (!forward_only && (j & 1)) ? 1 : 0;
   const bool ph = picp_use_pinhole(args->K);
 #define PICP_LAUNCH_R(VEC, PH)                                                                        \
   hipLaunchKernelGGL((picp_round_kernel<VEC, PH>), dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U, \
-                     V, *args, probs, blkinfo, st_in, st_out, part, tickets, j)
+                     V, *args, probs, blkinfo, st_in, st_out, part, tickets, j, rev)
   if (vec == 4) {
     if (ph) PICP_LAUNCH_R(4, 1); else PICP_LAUNCH_R(4, 0);
   } else if (vec == 1) {
