@@ -177,16 +177,24 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       constexpr int NG = PICP_PBLOCK / 32;  // block groups swept in parallel
       constexpr int MAXG = PICP_MAX_PBLK / NG;
       unsigned long long gv[MAXG];
-      bool ok = false;
-      for (;;) {
-        ok = true;
+      // re-poll only the granules whose tag has not matched yet: a full 50 KB sweep costs
+      // ~0.8 us at one block's share of the fabric, a re-poll of the few late blocks far less
+      unsigned pending = 0;
 #pragma unroll
-        for (int i = 0; i < MAXG; ++i) {
-          const int b = g + NG * i;
-          gv[i] = __hip_atomic_load(prob_part0 + (epoch & 1) * part_stride + (size_t)min(b, nblk - 1) * PICP_NPART + e, RLX_AGENT);
-          ok &= (b >= nblk) || ((unsigned)(gv[i] >> 32) == epoch);
-        }
-        if (ok) break;
+      for (int i = 0; i < MAXG; ++i) {
+        gv[i] = 0;
+        if (g + NG * i < nblk) pending |= 1u << i;
+      }
+      for (;;) {
+        const unsigned want = pending;  // issue every pending load before checking any tag
+#pragma unroll
+        for (int i = 0; i < MAXG; ++i)
+          if (want & (1u << i))
+            gv[i] = __hip_atomic_load(prob_part0 + (epoch & 1) * part_stride + (size_t)(g + NG * i) * PICP_NPART + e, RLX_AGENT);
+#pragma unroll
+        for (int i = 0; i < MAXG; ++i)
+          if ((want & (1u << i)) && (unsigned)(gv[i] >> 32) == epoch) pending &= ~(1u << i);
+        if (!pending) break;
         if (timed_out(deadline)) {
           __hip_atomic_store(errw, 1u, RLX_AGENT);
           break;
