@@ -424,3 +424,38 @@ def test_fast_reciprocal_is_correctly_rounded(native):
     it must equal the IEEE division bit for bit -- which, by power-of-two scaling, proves it
     for every |z| in [2^-100, 2^100] (outside: the kernels use the division)."""
     assert native.selftest_rcp(-8, 8) == 0
+
+
+@pytest.mark.parametrize("sizes", [[300003], [262147, 300001]])
+def test_streaming_sweep_directions_ragged_tail(native, oracle, sizes):
+    """Graph mode with float4 lanes (> 2^18 correspondences): odd rounds sweep each block's slice
+    backwards (change 7).  Slices whose tail is not a multiple of 4 exercise the
+    mirrored masking; both sweep orders must match the oracle, and each must replay bit-exactly."""
+    import os
+    synth = _synth()
+    probs = [synth.make_problem(n, seed=900 + i, outlier_frac=0.2, pixel_noise=0.5, shuffle=False)
+             for i, n in enumerate(sizes)]
+    xyz = np.concatenate([p["xyz"] for p in probs])
+    uv = np.concatenate([p["uv"] for p in probs])
+    Ti = np.stack([p["T_init"] for p in probs])
+    res = {}
+    for fwd in ("0", "1"):
+        os.environ["PICP_SWEEP_FORWARD"] = fwd
+        try:
+            b = _batch_mode(native, sizes, "graph")
+            assert b.info()["mode"] == "graph"
+            b.set_data(xyz, uv)
+            b.set_poses(Ti)
+            b.solve(threshold=THR, max_rounds=20, conv_eps=-1.0)
+            poses, stats = b.poses(), b.stats()
+            b.solve(threshold=THR, max_rounds=20, conv_eps=-1.0)
+            np.testing.assert_array_equal(b.poses(), poses)
+        finally:
+            os.environ.pop("PICP_SWEEP_FORWARD", None)
+        res[fwd] = (poses, stats)
+    for i, p in enumerate(probs):
+        T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"], p["y"], p["z"], p["u"],
+                                         p["v"], THR, mode=oracle.MODE_F64, max_rounds=20, conv_eps=-1.0)
+        for fwd, (poses, stats) in res.items():
+            assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL, (fwd, i)
+            assert abs(stats[i]["n_in"] - st_ref["n_in"]) <= 2, (fwd, i)
