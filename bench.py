@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--problems", type=int, default=0, help="override frames per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--skip-extras", action="store_true",
+                    help="only the timed solves (profiling runs: no convergence-enabled re-solve)")
     ap.add_argument("--frames", type=int, default=0, help="c5: sequence length (default 10000)")
     ap.add_argument("--obs", type=int, default=0, help="c5: observations per frame (default 2000)")
     ap.add_argument("--seg-len", type=int, default=40, help="c5: PICP steps per segment")
@@ -141,6 +143,9 @@ def main():
     corr_per_launch = int(info["total_corr"]) * (1 if info["mode"] == "graph" else R)
     achieved = BYTES_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
 
+    traffic, tsrc = (pmc_traffic("c2_persistent")
+                     if (args.workload == "c2" and n == 100000 and len(sizes) == 1 and R == 50
+                         and info["mode"] == "persistent") else (None, None))
     rounds_total = world * len(sizes) * R * args.steps
     value = rounds_total / elapsed
     out = {
@@ -171,7 +176,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": tsrc,
             "kernel": {"graph": "picp_round_kernel (one GN round per launch)",
                        "persistent": "picp_persistent_kernel (all GN rounds in one launch)",
                        "block": "picp_block_kernel (all GN rounds, one block per frame)"}[info["mode"]],
@@ -184,14 +190,49 @@ def main():
         },
         "pose_err_vs_gt_se3": err,
     }
+    if args.workload in ("c2", "c3") and not args.skip_extras:
+        # C2 is timed with exactly R rounds; also report the icp_test loop with its
+        # convergence test on (exec/icp_test.cpp:99-106), measured after the timed region
+        cparams = dict(params, conv_eps=1e-5)
+        b.solve(**cparams)
+        rounds_run = max(int(st["rounds"]) for st in b.stats())
+        cms, _ = b.time(args.steps, **cparams)
+        per_solve_ms = cms / args.steps
+        out["with_convergence"] = {
+            "conv_eps": 1e-5, "rounds_run": rounds_run, "ms_per_solve": round(per_solve_ms, 4),
+            "iterations_per_s": round(len(sizes) * rounds_run / (per_solve_ms * 1e-3), 1),
+            "pose_err_vs_gt_se3": max(synth.se3_log_norm(b.poses()[i], T_gt[i]) for i in range(len(sizes))),
+        }
     if args.workload == "c2" and args.stream_n > 0 and world == 1:
         out["roofline_streaming"] = streaming_roofline(args.stream_n, R, thr, local if world > 1 else 0)
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(xyz[: sizes[0]], uv[: sizes[0]], T_init[0], R, thr, args.cpu_seconds)
+        out["cpu_baseline_all_cores"] = cpu_baseline_mt(xyz[: sizes[0]], uv[: sizes[0]], T_init[0], R, thr,
+                                                        max(2.0, args.cpu_seconds / 2))
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(name, fetch_scale=2.0):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC passes of the same command
+    (profiles/rNN/<name>_pmc_{FETCH_SIZE,WRITE_SIZE}.json, written by tools/gpu_pmc*.sh from two
+    separate --pmc passes).  FETCH_SIZE x fetch_scale (gfx950: x2 for wide coalesced streams,
+    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB.  (None, None) when absent: bench.py
+    cannot collect PMC counters live."""
+    import glob
+    import json as _json
+    dirs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*")))
+    for d in reversed(dirs):
+        f, w = (os.path.join(d, "%s_pmc_%s.json" % (name, c)) for c in ("FETCH_SIZE", "WRITE_SIZE"))
+        if os.path.exists(f) and os.path.exists(w):
+            fk = _json.load(open(f))["FETCH_SIZE"]["mean"]
+            wk = _json.load(open(w))["WRITE_SIZE"]["mean"]
+            src = "%s (FETCH_SIZE %.1f KiB x %g + WRITE_SIZE %.1f KiB per launch)" % (
+                os.path.relpath(f, ROOT).replace("FETCH_SIZE", "{FETCH,WRITE}_SIZE"), fk, fetch_scale, wk)
+            return round((fk * fetch_scale + wk) * 1024.0), src
+    return None, None
 
 
 def streaming_roofline(n, R, thr, device):
@@ -212,11 +253,13 @@ def streaming_roofline(n, R, thr, device):
     per_launch = BYTES_PER_CORR * n * (1 if launches else R)
     achieved = per_launch / (launch_us * 1e-6) / 1e9
     err = synth.se3_log_norm(b.poses()[0], p["T_gt"])
+    traffic, tsrc = pmc_traffic("stream16m") if (n == 16000000 and launches) else (None, None)
     return {"bound": "hbm", "n_corr": n, "working_set_MB": round(BYTES_PER_CORR * n / 1e6, 1),
             "kernel": "picp_round_kernel (one GN round per launch)" if launches else info["mode"],
             "mode": info["mode"], "blocks_per_launch": info["n_blocks"], "kernel_us": round(launch_us, 3),
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "iterations_per_s": round(R * 5 / (ev_ms * 1e-3), 2),
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
+            "bytes_per_launch": per_launch, "iterations_per_s": round(R * 5 / (ev_ms * 1e-3), 2),
             "pose_err_vs_gt_se3": err}
 
 
@@ -310,7 +353,7 @@ def bench_vo(args, wl, world, rank, local, dist, torch):
         "pose_err_vs_gt_se3_max": stats[0],
         "pose_err_frame": "camera-in-world poses in each segment's frame (its first camera)",
     }
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out))
@@ -340,14 +383,48 @@ def cpu_baseline_vo(seq, L, budget_s):
             break
     return {"value": round(frames / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": "%d frames in %d-step segments of the same sequence (oracle VO loop, faithful "
-                      "float32, gcc -O2, 1 thread) in %.1f s" % (frames, L, el)}
+                      "float32, gcc -O3, 1 thread) in %.1f s" % (frames, L, el)}
+
+
+def _cpu_model():
+    import platform
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline_mt(xyz, uv, T_init, R, thr, budget_s):
+    """SURVEY.md §8d's all-cores CPU baseline for C2/C3: the oracle's loop with the linearize as a
+    chunked reduction over OMP_NUM_THREADS threads (the box's CPU share; os.cpu_count() shows the
+    whole machine).  Timing only; its pose is checked against the sequential oracle's."""
+    import numpy as np
+    import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    x, y, z = (np.ascontiguousarray(xyz[:, i]) for i in range(3))
+    u, v = np.ascontiguousarray(uv[:, 0]), np.ascontiguousarray(uv[:, 1])
+    Kref = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
+    solves, t0 = 0, time.perf_counter()
+    while True:
+        T_mt, _ = O.solve_soa_mt(T_init, Kref, 480, 640, x, y, z, u, v, thr, threads,
+                                 mode=O.MODE_FAITHFUL, max_rounds=R, conv_eps=-1.0)
+        solves += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(solves * R / el, 3), "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, "
+                      "linearize as a chunked reduction over %d OpenMP threads, gcc -O3 "
+                      "-march=x86-64-v3) in %.1f s on %s" % (solves, R, len(x), threads, el, _cpu_model())}
 
 
 def cpu_baseline(xyz, uv, T_init, R, thr, budget_s):
     """Oracle (faithful float32, sequential) single thread on one frame of the workload:
     whole R-round solves until the time budget is used (at least one)."""
-    import platform
-
     import numpy as np
     import oracle as O
     x, y, z = (np.ascontiguousarray(xyz[:, i]) for i in range(3))
@@ -362,17 +439,10 @@ def cpu_baseline(xyz, uv, T_init, R, thr, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    model = platform.processor() or ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
     return {"value": round(solves * R / el, 3), "unit": "iterations/s", "cores": 1, "kind": "port",
             "sample": "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, "
-                      "gcc -O2, 1 thread) in %.1f s on %s" % (solves, R, len(x), el, model)}
+                      "gcc -O3 -march=x86-64-v3, 1 thread) in %.1f s on %s" % (solves, R, len(x), el,
+                                                                              _cpu_model())}
 
 
 if __name__ == "__main__":

@@ -67,6 +67,10 @@ def lib():
                                    f, f, i, i, i, i, f, ctypes.POINTER(Stats),
                                    ctypes.POINTER(ctypes.c_int)]
         L.or_solve_soa.restype = i
+        L.or_solve_soa_mt.argtypes = [_f32p, _f32p, i, i, _f32p, _f32p, _f32p, _f32p, _f32p, i64,
+                                      f, f, i, i, i, i, f, i, ctypes.POINTER(Stats),
+                                      ctypes.POINTER(ctypes.c_int)]
+        L.or_solve_soa_mt.restype = i
         L.or_triangulate.argtypes = [_f32p, _f32p, _f32p, _f32p, i64, _f32p]
         L.or_projection_matrix.argtypes = [_f32p, _f32p, _f32p]
         L.or_iso_inverse.argtypes = [_f32p, _f32p]
@@ -176,6 +180,22 @@ def solve_soa(T, K, rows, cols, x, y, z, u, v, threshold, damping=1.0, min_inlie
                                 _f32(v), len(x), threshold, damping, min_inliers,
                                 int(keep_outliers), mode, max_rounds, conv_eps,
                                 ctypes.byref(st), ctypes.byref(conv))
+    return _pose44(p), {"chi_in": st.chi_in, "chi_out": st.chi_out, "n_in": st.n_in,
+                        "ok": st.ok, "rounds": rounds, "converged": bool(conv.value)}
+
+
+def solve_soa_mt(T, K, rows, cols, x, y, z, u, v, threshold, threads, damping=1.0, min_inliers=0,
+                 keep_outliers=False, mode=MODE_FAITHFUL, max_rounds=50, conv_eps=1e-5):
+    """solve_soa with the linearize as a chunked reduction over `threads` OpenMP threads.
+    TIMING ONLY (the all-cores CPU baseline of SURVEY.md §8d): the summation order is not the
+    reference's, so tests never use it as the parity oracle."""
+    p = _pose16(T)
+    st = Stats()
+    conv = ctypes.c_int(0)
+    rounds = lib().or_solve_soa_mt(p, _k9(K), rows, cols, _f32(x), _f32(y), _f32(z), _f32(u),
+                                   _f32(v), len(x), threshold, damping, min_inliers,
+                                   int(keep_outliers), mode, max_rounds, conv_eps, int(threads),
+                                   ctypes.byref(st), ctypes.byref(conv))
     return _pose44(p), {"chi_in": st.chi_in, "chi_out": st.chi_out, "n_in": st.n_in,
                         "ok": st.ok, "rounds": rounds, "converged": bool(conv.value)}
 

@@ -185,6 +185,42 @@ void or_linearize_soa(const float T[16], const float K[9], int rows, int cols,
   acc_out(&a, mode, out);
 }
 
+/* Chunked-reduction linearize for the all-cores CPU baseline (SURVEY.md §8d "a chunked
+ * reduction (C2/C3) on all host cores"): contiguous chunks, one per OpenMP thread, each
+ * accumulated exactly like or_linearize_soa, then combined in chunk order.  The summation order
+ * is not the reference's sequential one, so this is TIMING ONLY (bench.py cpu_baseline_mt),
+ * never a parity oracle. */
+#define OR_MT_MAX 256
+void or_linearize_soa_mt(const float T[16], const float K[9], int rows, int cols,
+                         const float* x, const float* y, const float* z, const float* u,
+                         const float* v, int64_t m, float threshold, int keep_outliers, int mode,
+                         int threads, or_lin_t* out) {
+  static acc_t parts[OR_MT_MAX];
+  const int nt = threads < 1 ? 1 : (threads > OR_MT_MAX ? OR_MT_MAX : threads);
+#pragma omp parallel for num_threads(nt) schedule(static, 1)
+  for (int t = 0; t < nt; ++t) {
+    acc_t a;
+    memset(&a, 0, sizeof(a));
+    const int64_t lo = m * t / nt, hi = m * (t + 1) / nt;
+    for (int64_t k = lo; k < hi; ++k) {
+      const float p[3] = {x[k], y[k], z[k]};
+      const float zz[2] = {u[k], v[k]};
+      acc_one(&a, T, K, rows, cols, p, zz, threshold, keep_outliers, mode);
+    }
+    parts[t] = a;
+  }
+  acc_t a = parts[0];
+  for (int t = 1; t < nt; ++t) {
+    const acc_t* b = &parts[t];
+    for (int i = 0; i < 36; ++i) { a.Hf[i] += b->Hf[i]; a.Hd[i] += b->Hd[i]; }
+    for (int i = 0; i < 6; ++i) { a.bf[i] += b->bf[i]; a.bd[i] += b->bd[i]; }
+    a.chi_in_f += b->chi_in_f; a.chi_out_f += b->chi_out_f;
+    a.chi_in_d += b->chi_in_d; a.chi_out_d += b->chi_out_d;
+    a.n_in += b->n_in; a.n_proj += b->n_proj;
+  }
+  acc_out(&a, mode, out);
+}
+
 /* Rx, Ry, Rz, v2tEuler: src/defs.h:100-136 (row-major 3x3 temporaries) */
 static void rot_x(float a, float R[3][3]) {
   float c = cosf(a), s = sinf(a);
@@ -418,6 +454,33 @@ int or_solve_soa(float T[16], const float K[9], int rows, int cols, const float*
 }
 
 /* P = K * (T_cw^-1)(0:3, 0:4), src/cam.cpp:109-112 ; row-major 3x4 out */
+/* or_solve_soa over the chunked-reduction linearize (timing only, see or_linearize_soa_mt). */
+int or_solve_soa_mt(float T[16], const float K[9], int rows, int cols, const float* x,
+                    const float* y, const float* z, const float* u, const float* v, int64_t m,
+                    float threshold, float damping, int min_inliers, int keep_outliers, int mode,
+                    int max_rounds, float conv_eps, int threads, or_stats_t* last_stats,
+                    int* converged) {
+  float prev = FLT_MAX;
+  int rounds = 0;
+  or_stats_t st;
+  memset(&st, 0, sizeof(st));
+  if (converged) *converged = 0;
+  for (int j = 0; j < max_rounds; ++j) {
+    or_lin_t lin;
+    or_linearize_soa_mt(T, K, rows, cols, x, y, z, u, v, m, threshold, keep_outliers, mode,
+                        threads, &lin);
+    int ok = round_tail(T, &lin, damping, min_inliers, mode, &st);
+    rounds++;
+    if (!ok) break;
+    if (conv_check(&prev, st.chi_in, conv_eps)) {
+      if (converged) *converged = 1;
+      break;
+    }
+  }
+  if (last_stats) *last_stats = st;
+  return rounds;
+}
+
 void or_projection_matrix(const float K[9], const float T_cw[16], float P[12]) {
   float Ti[16];
   or_iso_inverse(T_cw, Ti);

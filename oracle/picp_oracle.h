@@ -95,6 +95,19 @@ int or_solve_soa(float T[16], const float K[9], int rows, int cols, const float*
                  float threshold, float damping, int min_inliers, int keep_outliers, int mode,
                  int max_rounds, float conv_eps, or_stats_t* last_stats, int* converged);
 
+/* Timing-only variants for the all-cores CPU baseline: the linearize is a chunked reduction
+ * over `threads` OpenMP threads (contiguous chunks, combined in chunk order).  NOT a parity
+ * oracle: the summation order differs from the reference's sequential one. */
+void or_linearize_soa_mt(const float T[16], const float K[9], int rows, int cols,
+                         const float* x, const float* y, const float* z, const float* u,
+                         const float* v, int64_t m, float threshold, int keep_outliers, int mode,
+                         int threads, or_lin_t* out);
+int or_solve_soa_mt(float T[16], const float K[9], int rows, int cols, const float* x,
+                    const float* y, const float* z, const float* u, const float* v, int64_t m,
+                    float threshold, float damping, int min_inliers, int keep_outliers, int mode,
+                    int max_rounds, float conv_eps, int threads, or_stats_t* last_stats,
+                    int* converged);
+
 /* Linear (DLT) triangulation, OpenCV cv::triangulatePoints + convertPointsFromHomogeneous
  * as called from src/cam.cpp:115-118.  P1,P2 are 3x4 ROW-major (cv::Mat layout).
  * uv1/uv2 packed float2, xyz_out packed float3.  Smallest right singular vector via a

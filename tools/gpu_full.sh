@@ -8,6 +8,6 @@ tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python3 bench.py --no-cpu --steps 20 > gpurun_out/prof_c2.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_c2.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python3 bench.py --no-cpu --skip-extras --steps 20 > gpurun_out/prof_c2.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_c2.log; exit 1; }
 cat gpurun_out/prof_c2/run_kernel_stats.csv
 tail -1 gpurun_out/prof_c2.log

@@ -4,7 +4,7 @@
 # share a pass; gfx950 FETCH_SIZE counts half of a wide coalesced stream -> x2).
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="--no-cpu --steps 3 --warmup 1 --workload c2 --n ${N:-16000000} --stream-n 0"
+ARGS="--no-cpu --skip-extras --steps 3 --warmup 1 --workload c2 --n ${N:-16000000} --stream-n 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc/s16m_trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/s16m_trace.log 2>&1 || { echo trace failed; tail gpurun_out/pmc/s16m_trace.log; exit 1; }
 cat gpurun_out/pmc/s16m_trace/run_kernel_stats.csv
 for C in FETCH_SIZE WRITE_SIZE; do
