@@ -9,19 +9,33 @@
 // per round and no HBM re-read per round: a batch of frames is bound by VALU issue, not by
 // hand-off latency or HBM.  Ragged batches read (offset, n) from the problem
 // table.
+//
+// Split (split = 2): when twice the problems still fit on the chip (C4: 128 frames, 256 CUs),
+// each problem runs on TWO blocks, each with half of the correspondences, so no CU idles.  Per
+// round each block publishes its 32-term partial as 64 granules {round, hi|lo} (the double sum
+// as hi = (float)t, lo = (float)(t - hi)), polls its partner's, and both add the two halves in
+// block order: both run the identical solve, so no broadcast is needed.  Partners are blockIdx
+// b and b + 8, which round-robin placement puts on the same XCD (speed only: correctness rests
+// on the tags).  Granules are double-buffered by round parity and zeroed by a memset node before
+// every launch; every wait has an s_memrealtime deadline, refreshed each round (error word set,
+// the problem stops, the host reports it).
 #include "picp_device.h"
 
 using namespace picp;
 
 #define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs
 #define PICP_BLDS_ITEMS 7680  // items staged in LDS: 5 x 4 B x 7680 = 150 KB of the 160 KB per CU
+#define PICP_XG 64            // exchange granules per block per round: 32 hi + 32 lo
+
+typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
 
 template <int NPT, int PH>
 __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
-    PicpState* __restrict__ st_out, int lds_items) {
+    PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
+    unsigned long long* xg, unsigned int* err, unsigned long long timeout_ticks) {
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   __shared__ float s_wave[PICP_BBLOCK / 64][PICP_NPART];
   __shared__ double s_tot[PICP_NPART];
@@ -30,7 +44,13 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
   __shared__ PicpState s_st;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int p = blockIdx.x;
+  int p = blockIdx.x, h = 0;
+  if (split == 2) {  // partners b, b + 8 (same XCD); h = which half of the problem
+    const int s = (int)blockIdx.x >> 3;
+    h = s & 1;
+    p = ((s >> 1) << 3) + ((int)blockIdx.x & 7);
+    if (p >= n_problems) return;  // grid padding (whole pairs only)
+  }
   int64_t base;
   int n;
   if (A.uniform) {
@@ -41,6 +61,13 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     base = P.offset;
     n = P.n;
   }
+  if (split == 2) {  // halves start on a multiple of 4 (the planes' alignment)
+    const int half = (((n + 1) >> 1) + 3) & ~3;
+    const int first = min(n, h * half);
+    n = (h == 0) ? min(n, half) : n - first;
+    if (n > 0) base += first;  // an empty half keeps a valid base (its loads are clamped to it)
+  }
+  bgu64_t* const xgg = (bgu64_t*)xg;
 
   // the problem, loaded once into registers (coalesced: item = tid + k*BLOCK)
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
@@ -135,6 +162,34 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
       double t = 0.0;
 #pragma unroll
       for (int w = 0; w < PICP_BBLOCK / 64; ++w) t += (double)s_wave[w][tid];
+      if (split == 2) {
+        // publish {round, hi}, {round, lo}; poll the partner's; add the halves in block order
+        const float hi = (float)t, lo = (float)(t - (double)hi);
+        const size_t slot = (size_t)(round & 1) * gridDim.x;
+        bgu64_t* mine = xgg + (slot + blockIdx.x) * PICP_XG;
+        const bgu64_t* theirs = xgg + (slot + (blockIdx.x ^ 8u)) * PICP_XG;
+        const unsigned tag = (unsigned)round;
+        __hip_atomic_store(mine + tid, ((unsigned long long)tag << 32) | __float_as_uint(hi),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(mine + PICP_NPART + tid, ((unsigned long long)tag << 32) | __float_as_uint(lo),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
+        unsigned long long gh = 0, gl = 0;
+        for (;;) {
+          gh = __hip_atomic_load(theirs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          gl = __hip_atomic_load(theirs + PICP_NPART + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) break;
+          if (__builtin_amdgcn_s_memrealtime() > deadline) {
+            __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gh = gl = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const double mine_t = (double)hi + (double)lo;
+        const double their_t = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
+        t = (h == 0) ? mine_t + their_t : their_t + mine_t;
+      }
       s_tot[tid] = t;
     }
     __syncthreads();
@@ -144,6 +199,8 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
       for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
       PicpState ns;
       finish_round(A, s_st, tot, round, ns);
+      if (split == 2 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+        ns.done = 1;  // a partner wait timed out: stop (the host reports the error)
       s_st = ns;
 #pragma unroll
       for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
@@ -153,20 +210,29 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     }
     __syncthreads();
   }
-  if (tid < 32) reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
+  if (h == 0 && tid < 32)
+    reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
 }
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part
 
-// max_n: the largest problem of the launch (sizes the LDS stage: max_n - npt*512 items, capped)
-extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
+// max_n: the largest problem of the launch (sizes the LDS stage: max_n - npt*512 items, capped).
+// split = 1: grid = n_problems blocks.  split = 2: grid = round_up(2 * n_problems, 16) blocks, all
+// co-resident (the caller checks grid <= CUs), xg = 2 * grid * 64 zeroed u64 granules, err a
+// zeroed word.
+extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
-                                        PicpState* st_out, int max_n) {
-  if (grid <= 0 || !args) return hipErrorInvalidValue;
+                                        PicpState* st_out, int max_n, int split,
+                                        unsigned long long* xg, unsigned int* err,
+                                        unsigned long long timeout_ticks) {
+  if (n_problems <= 0 || !args || (split != 1 && split != 2)) return hipErrorInvalidValue;
+  if (split == 2 && (!xg || !err)) return hipErrorInvalidValue;
+  const int grid = (split == 2) ? ((2 * n_problems + 15) / 16) * 16 : n_problems;
+  const int per_block = (split == 2) ? ((((max_n + 1) >> 1) + 3) & ~3) : max_n;
   const bool ph = picp_use_pinhole(args->K);
-  const int lds_items = (max_n > npt * PICP_BBLOCK) ? min(max_n - npt * PICP_BBLOCK, PICP_BLDS_ITEMS) : 0;
+  const int lds_items = (per_block > npt * PICP_BBLOCK) ? min(per_block - npt * PICP_BBLOCK, PICP_BLDS_ITEMS) : 0;
   const size_t lds_bytes = (size_t)5 * lds_items * sizeof(float);
 #define PICP_LAUNCH_B(N)                                                                                  \
   if (ph) {                                                                                               \
@@ -174,13 +240,15 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, c
       hipFuncSetAttribute((const void*)picp_block_kernel<N, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                           (int)lds_bytes);                                                                \
     hipLaunchKernelGGL((picp_block_kernel<N, 1>), dim3(grid), dim3(PICP_BBLOCK), lds_bytes, stream, X, Y, \
-                       Z, U, V, *args, probs, st_in, st_out, lds_items);                                  \
+                       Z, U, V, *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err,       \
+                       timeout_ticks);                                                                    \
   } else {                                                                                                \
     if (lds_bytes > 65536)                                                                                \
       hipFuncSetAttribute((const void*)picp_block_kernel<N, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                           (int)lds_bytes);                                                                \
     hipLaunchKernelGGL((picp_block_kernel<N, 0>), dim3(grid), dim3(PICP_BBLOCK), lds_bytes, stream, X, Y, \
-                       Z, U, V, *args, probs, st_in, st_out, lds_items);                                  \
+                       Z, U, V, *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err,       \
+                       timeout_ticks);                                                                    \
   }
   switch (npt) {
     case 1: PICP_LAUNCH_B(1); break;

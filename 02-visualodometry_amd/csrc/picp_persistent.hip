@@ -15,7 +15,7 @@
 //   3. every other block polls the 16 pose granules (one wave), then starts the next round.
 // Correctness does not depend on placement or timing: only tags are trusted.  Blocks must be
 // co-resident (the host caps the grid at the CU count with ~110 VGPRs / 10 KB LDS per block),
-// every spin is bounded by an s_memrealtime deadline (timeout -> error word, loop exits), and
+// every spin is bounded by a per-round s_memrealtime deadline (timeout -> error word, loop exits), and
 // the host zeroes every granule with a memset node before each launch.
 #include "picp_device.h"
 
@@ -112,7 +112,6 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     if (leader && s.done) st_out[p] = s;
   }
   __syncthreads();
-  const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
 
   Cam C;
   C.k00 = A.K[0]; C.k10 = A.K[1]; C.k20 = A.K[2];
@@ -125,6 +124,9 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
   const bool keep = A.keep_outliers != 0;
 
   for (unsigned epoch = 1; !s_done; ++epoch) {
+    // every wait of this round is bounded from the round's start (a whole solve may take far
+    // longer than timeout_ticks at large max_rounds; one round never does)
+    const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
     // ---- 1. linearize the slice at the current pose, publish the block partial ----
     PSTAMP(0);
     Pose T;

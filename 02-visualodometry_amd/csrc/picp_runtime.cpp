@@ -33,11 +33,13 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              const PicpState* st_in, PicpState* st_out,
                                              unsigned long long* gpart, unsigned long long* gpose,
                                              unsigned int* err, unsigned long long timeout_ticks);
-extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
+extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
-                                        PicpState* st_out, int max_n);
+                                        PicpState* st_out, int max_n, int split,
+                                        unsigned long long* xg, unsigned int* err,
+                                        unsigned long long timeout_ticks);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_persistent_block(void);
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
@@ -176,6 +178,7 @@ struct picp_batch {
   int n_u = 0;
   int64_t stride_u = 0;
   int num_cu = 256;            // compute units of the device
+  int split = 1;               // block mode: blocks per problem (1, or 2 when 2*np fits the chip)
   int mode = PICP_MODE_GRAPH;  // PICP_MODE_GRAPH (launch per round) / PICP_MODE_PERSISTENT
   int npt = 1;                 // persistent: correspondences per lane held in registers
   unsigned char* sync = nullptr;   // persistent: [err 16 B | pose granules | partial granules]
@@ -195,6 +198,12 @@ struct picp_batch {
   float* U() const { return planes + 3 * plane_cap; }
   float* V() const { return planes + 4 * plane_cap; }
 };
+
+// persistent launches and split block launches hand off through granules and report a timed-out
+// wait in the error word at the head of b->sync
+static bool uses_err_word(const picp_batch* b) {
+  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split == 2);
+}
 
 static void drop_graph(picp_batch* b) {
   if (b->gexec) hipGraphExecDestroy(b->gexec);
@@ -296,10 +305,29 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     } else if (pnpt) {
       b->mode = PICP_MODE_PERSISTENT;
     }
+    b->split = 1;
     if (b->mode == PICP_MODE_PERSISTENT) {
       b->npt = pnpt;
       ipb = pnpt * picp_persistent_block();
     } else if (b->mode == PICP_MODE_BLOCK) {
+      // two blocks per problem when every pair still gets its own CUs (C4: 128 frames on 256 CUs)
+      // and the halves are big enough to pay for the per-round partner exchange;
+      // PICP_BLOCK_SPLIT=1|2 forces
+      int split = ((int64_t)2 * np <= b->num_cu && ((2 * np + 15) / 16) * 16 <= b->num_cu &&
+                   max_n >= 4096) ? 2 : 1;
+      if (const char* e = getenv("PICP_BLOCK_SPLIT")) {
+        const int v = atoi(e);
+        if (v == 1) split = 1;
+        if (v == 2 && ((2 * np + 15) / 16) * 16 <= b->num_cu) split = 2;
+      }
+      b->split = split;
+      if (split == 2) {  // register items per lane for a half
+        const int64_t half = round_up((max_n + 1) / 2, 4);
+        int cap = picp_block_max_items() / 512;
+        if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
+        bnpt = 1;
+        while (bnpt < cap && (int64_t)bnpt * 512 < half) bnpt *= 2;
+      }
       b->npt = bnpt;
     }
   }
@@ -356,8 +384,13 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     HIP_TRY(hipHostMalloc((void**)&b->st_pinned, (size_t)np * sizeof(PicpState), hipHostMallocDefault));
     b->np_cap = np;
   }
-  if (b->mode == PICP_MODE_PERSISTENT) {
-    b->sync_bytes = (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8, 256);
+  if (b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split == 2)) {
+    // persistent: error word | pose granules | partial granules (x2 parities);
+    // split block: error word | exchange granules (x2 parities, 64 per block)
+    const int64_t sgrid = ((2 * (int64_t)np + 15) / 16) * 16;
+    b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
+                        ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8, 256)
+                        : (size_t)round_up(16 + 2 * sgrid * 64 * 8, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
       b->sync = nullptr;
@@ -453,9 +486,19 @@ static hipError_t graph_prologue(picp_batch* b) {
 // Enqueue a fused R-round solve on the stream: block / persistent mode one launch; graph mode
 // the initial-state copy, the ticket memset and R round launches.
 static hipError_t enqueue_solve(picp_batch* b, int R) {
-  if (b->mode == PICP_MODE_BLOCK)
+  if (b->mode == PICP_MODE_BLOCK) {
+    unsigned int* err = nullptr;
+    unsigned long long* xg = nullptr;
+    if (b->split == 2) {  // every exchange granule and the error word zeroed before each launch
+      hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
+      if (e != hipSuccess) return e;
+      err = reinterpret_cast<unsigned int*>(b->sync);
+      xg = reinterpret_cast<unsigned long long*>(b->sync + 16);
+    }
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
-                             b->probs_d, b->init_d, b->st_d[0], (int)b->max_n);
+                             b->probs_d, b->init_d, b->st_d[0], (int)b->max_n, b->split, xg, err,
+                             b->timeout_ticks);
+  }
   if (b->mode == PICP_MODE_PERSISTENT) {
     // every polled word (error word and all granules) is zeroed before each launch
     hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
@@ -500,7 +543,7 @@ static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
   b->last_rounds = R;
   b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
-  b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
+  b->last_persistent = uses_err_word(b);
   return PICP_OK;
 }
 
@@ -512,7 +555,7 @@ static int batch_read_results(picp_batch* b) {
     HIP_TRY(hipMemcpyAsync(&err, b->sync, sizeof(err), hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   memcpy(b->result_h.data(), b->st_pinned, (size_t)b->np * sizeof(PicpState));
-  if (err) return set_err(PICP_ERR_DEVICE, "persistent solve: a hand-off wait timed out (code %u)", err);
+  if (err) return set_err(PICP_ERR_DEVICE, "solve: a cross-block hand-off wait timed out (code %u)", err);
   return PICP_OK;
 }
 
@@ -682,7 +725,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
   if (total_ms) *total_ms = ms;
   b->last_rounds = R;
   b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
-  b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
+  b->last_persistent = uses_err_word(b);
   if (kernel_us) {
     // [0]: mean launch period of the round kernel inside the replayed graphs (event time over
     //      the timed replays / kernel launches; the graphs are back-to-back launches, so this is
@@ -707,7 +750,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
       hipEventDestroy(e0);
       hipEventDestroy(e1);
       b->result_idx = 0;
-      b->last_persistent = (b->mode == PICP_MODE_PERSISTENT);
+      b->last_persistent = uses_err_word(b);
       return batch_read_results(b);
     }
     std::vector<hipEvent_t> ev((size_t)(R + 1));

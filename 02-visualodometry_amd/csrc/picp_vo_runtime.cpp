@@ -30,11 +30,13 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted);
 extern "C" int picp_match_prep_kch(int dim);
-extern "C" hipError_t picp_launch_block(hipStream_t stream, int grid, int npt, const float* X,
+extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
-                                        PicpState* st_out, int max_n);
+                                        PicpState* st_out, int max_n, int split,
+                                        unsigned long long* xg, unsigned int* err,
+                                        unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
 
@@ -340,7 +342,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
     if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
     if (e == hipSuccess)
       e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,
-                            V.st_in, (PicpState*)V.st_out, (int)h->max_obs);
+                            V.st_in, (PicpState*)V.st_out, (int)h->max_obs, 1, nullptr, nullptr, 0);
     if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &V, t);
   }
   return e;

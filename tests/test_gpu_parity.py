@@ -459,3 +459,44 @@ def test_streaming_sweep_directions_ragged_tail(native, oracle, sizes):
         for fwd, (poses, stats) in res.items():
             assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL, (fwd, i)
             assert abs(stats[i]["n_in"] - st_ref["n_in"]) <= 2, (fwd, i)
+
+
+@pytest.mark.parametrize("sizes", [[5000, 1, 3, 4097, 12000, 7], [10000] * 32])
+def test_block_split_matches_oracle(native, oracle, sizes):
+    """Block mode with two blocks per problem (PICP_BLOCK_SPLIT=2, the C4 layout: halves on
+    partner blocks that exchange {round, hi|lo} granules every round) and with one block per
+    problem: both vs the oracle, converged-round counts equal, replays bit-identical.  Problems
+    of 1-7 correspondences leave the second half empty."""
+    import os
+    synth = _synth()
+    probs = [synth.make_problem(n, seed=1300 + i, outlier_frac=0.1 if n >= 1000 else 0.0, pixel_noise=0.5,
+                                shuffle=False) for i, n in enumerate(sizes)]
+    xyz = np.concatenate([p["xyz"] for p in probs])
+    uv = np.concatenate([p["uv"] for p in probs])
+    Ti = np.stack([p["T_init"] for p in probs])
+    res = {}
+    for split in ("1", "2"):
+        os.environ["PICP_BLOCK_SPLIT"] = split
+        try:
+            b = _batch_mode(native, sizes, "block")
+            assert b.info()["mode"] == "block"
+            b.set_data(xyz, uv)
+            b.set_poses(Ti)
+            b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
+            poses, stats = b.poses(), b.stats()
+            b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
+            np.testing.assert_array_equal(b.poses(), poses)
+        finally:
+            os.environ.pop("PICP_BLOCK_SPLIT", None)
+        res[split] = (poses, stats)
+    for i, p in enumerate(probs):
+        if i >= 8 and i % 8:  # the uniform batch: every 8th problem against the oracle
+            continue
+        T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"], p["y"], p["z"], p["u"],
+                                         p["v"], THR, mode=oracle.MODE_F64, max_rounds=50, conv_eps=1e-5)
+        n = sizes[i]
+        for split, (poses, stats) in res.items():
+            assert synth.se3_log_norm(poses[i], T_ref) < _pose_tol(n), (split, i)
+            assert abs(stats[i]["n_in"] - st_ref["n_in"]) <= 2, (split, i)
+            if n >= 1000:
+                assert stats[i]["converged"] == int(st_ref["converged"]), (split, i)
