@@ -143,8 +143,12 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     }
     for (int i = tid; i < n_lds; i += 2 * PICP_BBLOCK) {  // LDS-staged items, in pairs
       const int i2 = min(i + PICP_BBLOCK, n_lds - 1);
-      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){lx[i], lx[i2]}, (f2){ly[i], ly[i2]}, (f2){lz[i], lz[i2]},
-                      (f2){lu[i], lu[i2]}, (f2){lv[i], lv[i2]}, true, i + PICP_BBLOCK < n_lds, a);
+      // scalar locals first: building the f2 operands from the LDS reads directly made the
+      // compiler round-trip them through scratch every round
+      const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
+      const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
+      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
+                      (f2){v0, v1}, true, i + PICP_BBLOCK < n_lds, a);
     }
     for (int i = r0 + n_lds + tid; i < n; i += 2 * PICP_BBLOCK) {  // streamed remainder
       const int i2 = min(i + PICP_BBLOCK, n - 1);

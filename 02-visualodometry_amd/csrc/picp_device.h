@@ -642,7 +642,18 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
 // Runs in one lane; everything is indexed by compile-time constants.
 __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState& s,
                                              const double* tot, int j, PicpState& ns) {
-  ns = s;
+  // field-wise, padding zeroed: a whole-struct copy of an LDS state kept its 44-byte tail in a
+  // scratch alloca (SROA cannot split the memcpy), a round trip on every round's critical path
+#pragma unroll
+  for (int i = 0; i < 9; ++i) ns.R[i] = s.R[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ns.t[i] = s.t[i];
+  ns.chi_prev = s.chi_prev;
+  ns.done = s.done;
+  ns.ok = s.ok;
+  ns.converged = s.converged;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) ns.pad[i] = 0;
   ns.chi_in = (float)tot[PICP_P_CHI_IN];
   ns.chi_out = (float)tot[PICP_P_CHI_OUT];
   ns.n_in = (int32_t)tot[PICP_P_N_IN];
