@@ -188,9 +188,41 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 }
 
 // The pre-filter kernel.  q_*/r_* prep arrays are indexed like the fp32 descriptors.  The
-// references stream through LDS in tiles of MM_RT, double-buffered: one barrier per tile, the
-// next tile's 16-B rows fetched into registers while this one is computed.
+// references stream through LDS in tiles of MM_RT, double-buffered: the next tile is fetched into
+// registers (16 B per lane) while this one is computed and stashed after it.  Rows past the end
+// are loaded clamped and masked in registers (norm := +inf).  LDS-DMA (global_load_lds) staging
+// was measured 30-40 % slower at full occupancy (C5, 4 blocks per CU: other blocks already hide
+// the fetch latency; profiles/r01/match_ab.log).
 #define MM_RT 128
+// Diagnostic build only (-DPICP_STAMPS): [0] queries through the full-scan fallback, [1] total
+// candidates rescanned, [2] queries, [3] max candidates of a query (tools/match_stats.py).
+#ifdef PICP_STAMPS
+__device__ unsigned long long picp_match_stats[4];
+extern "C" hipError_t picp_debug_match_stats(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_match_stats), sizeof(picp_match_stats), 0,
+                                     hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(picp_match_stats), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  return e;
+}
+#endif
+
+// min(a, b, c) for values that are never NaN (D' = n1 - 2 q.r of finite fp16 products, or +inf):
+// one v_min3_f32 -- fminf would add an IEEE canonicalisation (v_max x,x,x) per operand
+__device__ __forceinline__ float mm_min3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// m = 2m + (d <= t): the candidate bitmask in two instructions (compare into VCC, shift in as the
+// carry); after 16 steps bit 15-i holds element i
+__device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t) {
+  asm("v_cmp_le_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(m) : "v"(d), "v"(t) : "vcc");
+  return m;
+}
+
 template <int KCH>
 __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
@@ -201,13 +233,23 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     float* __restrict__ second_dist, int32_t* __restrict__ accepted) {
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
-  constexpr int CPT = (CH + MM_BLOCK - 1) / MM_BLOCK;  // chunks per thread
+  constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
+  static_assert(CH % MM_BLOCK == 0 && 2 * MM_RT == MM_BLOCK, "tile / block shape");
   constexpr int DMAX = 16 * KCH;
-  __shared__ mm_half8 s_t[2][CH];                   // tile rows, 16-B chunks: row*(DP/8) + c*2 + h
-  __shared__ float s_n[2][2][MM_RT];                // [buf][n1|n2][ref]
-  __shared__ int s_cnt[MM_WAVES][MM_QPW];
-  __shared__ int s_list[MM_WAVES][MM_QPW][MM_CAP];
-  __shared__ float s_nq[MM_WAVES][MM_QPW];
+  // all of the kernel's LDS in one __shared__ object
+  struct Lds {
+    mm_half8 t[2][CH];                   // tile rows, 16-B chunks: row*(DP/8) + c*2 + h
+    float n[2][2][MM_RT];                // [buf][n1|n2][ref]
+    int cnt[MM_WAVES][MM_QPW];
+    int list[MM_WAVES][MM_QPW][MM_CAP];
+    float nq[MM_WAVES][MM_QPW];
+  };
+  __shared__ Lds lds;
+  auto& s_t = lds.t;
+  auto& s_n = lds.n;
+  auto& s_cnt = lds.cnt;
+  auto& s_list = lds.list;
+  auto& s_nq = lds.nq;
 
   const MatchProblem P = probs[blockIdx.y];
   const int64_t q0 = (int64_t)blockIdx.x * MM_QPB;
@@ -230,33 +272,28 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   }
 
   const int64_t nr_all = P.nr;
-  const mm_half8* rsrc = reinterpret_cast<const mm_half8*>(r_h + P.r_off * DP);
-  // register staging of one tile: CPT chunks + this thread's norms (threads < MM_RT)
-  mm_half8 st[CPT];
-  float sn1 = INFINITY, sn2 = INFINITY;
+  // fetch tile t0 into registers (chunk tid + k*MM_BLOCK; the tile's norms: threads < MM_RT n1,
+  // the others n2), stash them into buffer b
+  mm_half8 stg[CPT];
+  float sn = INFINITY;
   auto fetch = [&](int64_t t0) {
-    const int64_t nt = min((int64_t)MM_RT, nr_all - t0);
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int ch = tid + k * MM_BLOCK;
-      const int64_t row = ch / (DP / 8);
-      st[k] = (ch < CH && row < nt) ? rsrc[t0 * (DP / 8) + ch] : mm_half8{};
+      const int64_t row = min(t0 + ch / (DP / 8), nr_all - 1);
+      stg[k] = *reinterpret_cast<const mm_half8*>(r_h + (P.r_off + row) * DP + (ch % (DP / 8)) * 8);
     }
-    if (tid < MM_RT) {
-      sn1 = (tid < nt) ? r_n1[P.r_off + t0 + tid] : INFINITY;  // past the end: excluded ...
-      sn2 = (tid < nt) ? r_n2[P.r_off + t0 + tid] : INFINITY;  // ... and never a candidate
-    }
+    const int nt = (tid < MM_RT) ? tid : tid - MM_RT;
+    sn = ((tid < MM_RT) ? r_n1 : r_n2)[P.r_off + min(t0 + nt, nr_all - 1)];
   };
-  auto stash = [&](int buf) {
+  auto stash = [&](int b) {
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int ch = tid + k * MM_BLOCK;
-      if (ch < CH) s_t[buf][ch] = st[k];
-    }
-    if (tid < MM_RT) {
-      s_n[buf][0][tid] = sn1;
-      s_n[buf][1][tid] = sn2;
-    }
+    for (int k = 0; k < CPT; ++k) s_t[b][tid + k * MM_BLOCK] = stg[k];
+    (&s_n[b][0][0])[tid] = sn;
+  };
+  auto load_b = [&](int b, int col, mm_half8* bb) {
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) bb[c] = s_t[b][col * (DP / 8) + 2 * c + hf];
   };
 
   // ---------------- pass 1: an upper bound on the approximate second-best D' per row ----------
@@ -273,24 +310,31 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   stash(0);
   int buf = 0;
   for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
-    __syncthreads();                                 // tile t0 in s_t[buf]; s_t[buf^1] free
+    __syncthreads();
     const bool more = t0 + MM_RT < nr_all;
     if (more) fetch(t0 + MM_RT);
 #pragma unroll 1
-    for (int sub = 0; sub < MM_RT / 32; ++sub) {  // rolled: two accumulators live, not eight
-      const int col = sub * 32 + r;
-      mm_half8 bb[KCH];
-#pragma unroll
-      for (int c = 0; c < KCH; ++c) bb[c] = s_t[buf][col * (DP / 8) + 2 * c + hf];
-      const float n1 = s_n[buf][0][col];
-      rmax = (n1 < INFINITY) ? fmaxf(rmax, n1) : rmax;
+    for (int sub = 0; sub < MM_RT / 32; sub += 2) {  // two column blocks per step: one min3 per row
+      const int ca = sub * 32 + r, cb = ca + 32;
+      mm_half8 ba[KCH], bbv[KCH];
+      load_b(buf, ca, ba);
+      load_b(buf, cb, bbv);
+      float na = s_n[buf][0][ca], nb = s_n[buf][0][cb];
+      na = (t0 + ca < nr_all) ? na : INFINITY;  // past the end: excluded
+      nb = (t0 + cb < nr_all) ? nb : INFINITY;
+      rmax = (na < INFINITY && na > rmax) ? na : rmax;
+      rmax = (nb < INFINITY && nb > rmax) ? nb : rmax;
 #pragma unroll
       for (int rb = 0; rb < MM_RB; ++rb) {
-        mm_f16v acc = {};
+        mm_f16v acc_a = {}, acc_b = {};
 #pragma unroll
-        for (int c = 0; c < KCH; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bb[c], acc, 0, 0, 0);
+        for (int c = 0; c < KCH; ++c) {
+          acc_a = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], ba[c], acc_a, 0, 0, 0);
+          acc_b = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bbv[c], acc_b, 0, 0, 0);
+        }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) b1[rb][i] = fminf(b1[rb][i], fmaf(-2.0f, acc[i], n1));  // n1 = inf: excluded
+        for (int i = 0; i < 16; ++i)  // n = inf: excluded
+          b1[rb][i] = mm_min3(b1[rb][i], fmaf(-2.0f, acc_a[i], na), fmaf(-2.0f, acc_b[i], nb));
       }
     }
     if (more) stash(buf ^ 1);
@@ -319,7 +363,22 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     }
 
   // ---------------- pass 2: collect the candidates ----------------
-  __syncthreads();
+  // Candidates are buffered per lane in registers and appended to the LDS lists after the pass
+  // (no LDS atomic round trip inside the MFMA loop); a lane whose buffer is full flushes it early
+  // (rare: 2.2 candidates per query on C5, tools/match_stats.py).
+  constexpr int MM_LB = 4;
+  int c_row[MM_LB], c_ref[MM_LB];
+  int c_n = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < MM_LB; ++k)
+      if (k < c_n) {
+        const int slot = atomicAdd(&s_cnt[w][c_row[k]], 1);
+        if (slot < MM_CAP) s_list[w][c_row[k]][slot] = c_ref[k];
+      }
+    c_n = 0;
+  };
+  __syncthreads();  // every wave is past pass 1's last tile before buffer 0 is refilled
   fetch(0);
   stash(0);
   buf = 0;
@@ -328,12 +387,12 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     const bool more = t0 + MM_RT < nr_all;
     if (more) fetch(t0 + MM_RT);
 #pragma unroll 1
-    for (int sub = 0; sub < MM_RT / 32; ++sub) {  // rolled: two accumulators live, not eight
+    for (int sub = 0; sub < MM_RT / 32; ++sub) {
       const int col = sub * 32 + r;
       mm_half8 bb[KCH];
-#pragma unroll
-      for (int c = 0; c < KCH; ++c) bb[c] = s_t[buf][col * (DP / 8) + 2 * c + hf];
-      const float n2 = s_n[buf][1][col];  // -inf: forced candidate; +inf: past the end
+      load_b(buf, col, bb);
+      float n2 = s_n[buf][1][col];  // -inf: forced candidate
+      n2 = (t0 + col < nr_all) ? n2 : INFINITY;  // past the end: never a candidate
 #pragma unroll
       for (int rb = 0; rb < MM_RB; ++rb) {
         mm_f16v acc = {};
@@ -341,18 +400,26 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
         for (int c = 0; c < KCH; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bb[c], acc, 0, 0, 0);
         unsigned m = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) m |= (fmaf(-2.0f, acc[i], n2) <= tau[rb][i]) ? (1u << i) : 0u;
-        while (m) {  // rare: the few candidates of this lane's 16 rows
-          const int i = __builtin_ctz(m);
+        for (int i = 0; i < 16; ++i) m = mm_shift_in_le(m, fmaf(-2.0f, acc[i], n2), tau[rb][i]);
+        while (m) {  // rare: the few candidates of this lane's 16 rows (bit 15-i = element i)
+          const int i = 15 - __builtin_ctz(m);
           m &= m - 1;
+          if (c_n == MM_LB) flush();
           const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
-          const int slot = atomicAdd(&s_cnt[w][row], 1);
-          if (slot < MM_CAP) s_list[w][row][slot] = (int)(t0 + col);
+#pragma unroll
+          for (int k = 0; k < MM_LB; ++k)  // register-indexed append (no scratch)
+            if (k == c_n) {
+              c_row[k] = row;
+              c_ref[k] = (int)(t0 + col);
+            }
+          ++c_n;
         }
       }
     }
     if (more) stash(buf ^ 1);
   }
+  __syncthreads();
+  flush();
   __syncthreads();
 
   // ---------------- exact update over the candidates, in index order ----------------
@@ -364,6 +431,12 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     float best = FLT_MAX, second = FLT_MAX;  // :78-79
     int32_t bi = -1;
     const int n = s_cnt[w][lane];
+#ifdef PICP_STAMPS
+    atomicAdd(&picp_match_stats[2], 1ull);
+    atomicAdd(&picp_match_stats[1], (unsigned long long)n);
+    atomicMax(&picp_match_stats[3], (unsigned long long)n);
+    if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) atomicAdd(&picp_match_stats[0], 1ull);
+#endif
     if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) {  // slow path: the reference's full scan
       for (int64_t j = 0; j < P.nr; ++j) {
         const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
