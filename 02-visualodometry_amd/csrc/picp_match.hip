@@ -193,7 +193,9 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 // are loaded clamped and masked in registers (norm := +inf).  LDS-DMA (global_load_lds) staging
 // was measured 30-40 % slower at full occupancy (C5, 4 blocks per CU: other blocks already hide
 // the fetch latency; profiles/r01/match_ab.log).
-#define MM_RT 128
+#ifndef MM_RT
+#define MM_RT 256  // reference rows per LDS tile (128: -3.4 % on C5, 512: -7 %; profiles/r01/match_ab.log)
+#endif
 // Diagnostic build only (-DPICP_STAMPS): [0] queries through the full-scan fallback, [1] total
 // candidates rescanned, [2] queries, [3] max candidates of a query (tools/match_stats.py).
 #ifdef PICP_STAMPS
@@ -234,7 +236,8 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
   constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
-  static_assert(CH % MM_BLOCK == 0 && 2 * MM_RT == MM_BLOCK, "tile / block shape");
+  constexpr int NPN = 2 * MM_RT / MM_BLOCK;        // norms per thread per tile (n1 | n2)
+  static_assert(CH % MM_BLOCK == 0 && (2 * MM_RT) % MM_BLOCK == 0, "tile / block shape");
   constexpr int DMAX = 16 * KCH;
   // all of the kernel's LDS in one __shared__ object
   struct Lds {
@@ -272,10 +275,10 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   }
 
   const int64_t nr_all = P.nr;
-  // fetch tile t0 into registers (chunk tid + k*MM_BLOCK; the tile's norms: threads < MM_RT n1,
-  // the others n2), stash them into buffer b
+  // fetch tile t0 into registers (chunk tid + k*MM_BLOCK; norm tid + k*MM_BLOCK of the tile's
+  // [n1 | n2] block), stash them into buffer b
   mm_half8 stg[CPT];
-  float sn = INFINITY;
+  float sn[NPN];
   auto fetch = [&](int64_t t0) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -283,13 +286,17 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
       const int64_t row = min(t0 + ch / (DP / 8), nr_all - 1);
       stg[k] = *reinterpret_cast<const mm_half8*>(r_h + (P.r_off + row) * DP + (ch % (DP / 8)) * 8);
     }
-    const int nt = (tid < MM_RT) ? tid : tid - MM_RT;
-    sn = ((tid < MM_RT) ? r_n1 : r_n2)[P.r_off + min(t0 + nt, nr_all - 1)];
+#pragma unroll
+    for (int k = 0; k < NPN; ++k) {
+      const int idx = tid + k * MM_BLOCK, nt = idx % MM_RT;
+      sn[k] = ((idx < MM_RT) ? r_n1 : r_n2)[P.r_off + min(t0 + nt, nr_all - 1)];
+    }
   };
   auto stash = [&](int b) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) s_t[b][tid + k * MM_BLOCK] = stg[k];
-    (&s_n[b][0][0])[tid] = sn;
+#pragma unroll
+    for (int k = 0; k < NPN; ++k) (&s_n[b][0][0])[tid + k * MM_BLOCK] = sn[k];
   };
   auto load_b = [&](int b, int col, mm_half8* bb) {
 #pragma unroll
