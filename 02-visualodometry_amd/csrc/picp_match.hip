@@ -140,8 +140,10 @@ extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int6
 typedef _Float16 mm_half8 __attribute__((ext_vector_type(8)));
 typedef float mm_f16v __attribute__((ext_vector_type(16)));
 
-#define MM_BLOCK 256
+#ifndef MM_WAVES
 #define MM_WAVES 4
+#endif
+#define MM_BLOCK (64 * MM_WAVES)
 #define MM_RB 1                   // 32-query MFMA row blocks per wave (share every B operand)
 #define MM_QPW (32 * MM_RB)       // queries per wave
 #define MM_QPB (MM_WAVES * MM_QPW)
