@@ -144,7 +144,9 @@ typedef float mm_f16v __attribute__((ext_vector_type(16)));
 #define MM_WAVES 4
 #endif
 #define MM_BLOCK (64 * MM_WAVES)
+#ifndef MM_RB
 #define MM_RB 1                   // 32-query MFMA row blocks per wave (share every B operand)
+#endif
 #define MM_QPW (32 * MM_RB)       // queries per wave
 #define MM_QPB (MM_WAVES * MM_QPW)
 #define MM_CAP 16                 // candidate slots per query
