@@ -33,6 +33,7 @@ class VOData:
         self.rows = int(d["rows"])
         self.ref_errors = d["ref_errors"] if "ref_errors" in d else None
         self.ref_map_ids = d["ref_map_ids"] if "ref_map_ids" in d else None
+        self.ref_trajectory = d["ref_trajectory"] if "ref_trajectory" in d else None
         self.cols = int(d["cols"])
         self.n_frames = self.gt_pose.shape[0]
         self._id2row = {int(i): r for r, i in enumerate(self.world_id)}
@@ -78,6 +79,18 @@ class VOData:
         off = np.zeros(self.n_frames + 1, np.int64)
         off[1:] = np.cumsum(np.bincount(self.meas_frame, minlength=self.n_frames))
         return off, np.ascontiguousarray(self.meas_uv[order]), np.ascontiguousarray(self.meas_desc[order])
+
+    def trajectory_rows(self, poses):
+        """The reference's output/estimated_trajectory.txt rows for camera-in-world poses
+        (exec/icp_test.cpp:140-182): frame, x, y of cameraToImage * pose (src/cam.cpp:18-26)
+        and the heading atan2(R10, R00) + pi/2."""
+        c2i = np.zeros((4, 4))
+        c2i[0, 2], c2i[1, 0], c2i[2, 1], c2i[3, 3] = 1.0, -1.0, -1.0, 1.0
+        rows = []
+        for k, T in enumerate(poses):
+            P = c2i @ np.asarray(T, np.float64)
+            rows.append((k, P[0, 3], P[1, 3], np.arctan2(P[1, 0], P[0, 0]) + np.pi / 2))
+        return np.array(rows)
 
     def map_ids(self, map_desc):
         """id_real of map points by exact descriptor identity with world.dat (noise-free data)."""

@@ -71,6 +71,19 @@ def lib():
                                       f, f, i, i, i, i, f, i, ctypes.POINTER(Stats),
                                       ctypes.POINTER(ctypes.c_int)]
         L.or_solve_soa_mt.restype = i
+        _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+        u64, d = ctypes.c_uint64, ctypes.c_double
+        L.or_five_point.argtypes = [_f64p, _f64p, _f64p]
+        L.or_five_point.restype = i
+        L.or_essential_samples.argtypes = [i, i, _i32p]
+        L.or_essential_samples.restype = i
+        L.or_ransac_update_iters.argtypes = [d, d, i, i]
+        L.or_ransac_update_iters.restype = i
+        L.or_find_essential.argtypes = [_f32p, _f32p, i, _f64p, d, d, i, _f64p, _i32p, _f64p]
+        L.or_find_essential.restype = i
+        L.or_decompose_essential.argtypes = [_f64p, _f64p, _f64p, _f64p]
+        L.or_recover_pose.argtypes = [_f64p, _f32p, _f32p, i, _f64p, d, _f64p, _f64p, _f64p, _u8p]
+        L.or_recover_pose.restype = i
         L.or_triangulate.argtypes = [_f32p, _f32p, _f32p, _f32p, i64, _f32p]
         L.or_projection_matrix.argtypes = [_f32p, _f32p, _f32p]
         L.or_iso_inverse.argtypes = [_f32p, _f32p]
@@ -198,6 +211,49 @@ def solve_soa_mt(T, K, rows, cols, x, y, z, u, v, threshold, threads, damping=1.
                                    ctypes.byref(st), ctypes.byref(conv))
     return _pose44(p), {"chi_in": st.chi_in, "chi_out": st.chi_out, "n_in": st.n_in,
                         "ok": st.ok, "rounds": rounds, "converged": bool(conv.value)}
+
+
+def five_point(q1, q2):
+    """Nister's five-point solver on 5 normalised correspondences -> list of 3x3 E (unit norm)."""
+    Es = np.zeros(90, np.float64)
+    n = lib().or_five_point(np.ascontiguousarray(q1, np.float64).reshape(-1),
+                            np.ascontiguousarray(q2, np.float64).reshape(-1), Es)
+    return [Es[9 * k:9 * k + 9].reshape(3, 3) for k in range(n)]
+
+
+def essential_samples(n, max_iters=1000):
+    """OpenCV RANSAC's subsets (its cv::RNG((uint64)-1) stream): (max_iters, 5) indices."""
+    idx = np.zeros(5 * max_iters, np.int32)
+    lib().or_essential_samples(int(n), int(max_iters), idx)
+    return idx.reshape(-1, 5)
+
+
+def find_essential(p1, p2, K, prob=0.999, threshold=1.0, max_iters=1000):
+    """cv::findEssentialMat(p1, p2, K, RANSAC, prob, threshold, max_iters) restated (see
+    picp_essential.c): -> (E 3x3 or None, inlier count)."""
+    p1 = _f32(p1).reshape(-1, 2)
+    p2 = _f32(p2).reshape(-1, 2)
+    Kv = np.array([K[0][0], K[1][1], K[0][2], K[1][2]], np.float64)
+    E = np.zeros(9, np.float64)
+    scratch = np.zeros(4 * max(len(p1), 1), np.float64)
+    idx = np.zeros(5 * max(max_iters, 1), np.int32)
+    cnt = lib().or_find_essential(p1.reshape(-1), p2.reshape(-1), len(p1), Kv, float(prob), float(threshold),
+                                  int(max_iters), scratch, idx, E)
+    return (E.reshape(3, 3) if cnt > 0 else None), cnt
+
+
+def recover_pose(E, p1, p2, K, dist=50.0):
+    """cv::recoverPose(E, p1, p2, K, R, t, dist, mask) restated: -> (R 3x3, t (3,), mask bool, count)."""
+    p1 = _f32(p1).reshape(-1, 2)
+    p2 = _f32(p2).reshape(-1, 2)
+    Kv = np.array([K[0][0], K[1][1], K[0][2], K[1][2]], np.float64)
+    R = np.zeros(9, np.float64)
+    t = np.zeros(3, np.float64)
+    mask = np.zeros(max(len(p1), 1), np.uint8)
+    scratch = np.zeros(4 * max(len(p1), 1), np.float64)
+    cnt = lib().or_recover_pose(np.ascontiguousarray(E, np.float64).reshape(-1), p1.reshape(-1), p2.reshape(-1),
+                                len(p1), Kv, float(dist), scratch, R, t, mask)
+    return R.reshape(3, 3), t, mask[:len(p1)].astype(bool), cnt
 
 
 def ldlt_solve6(A, rhs, double=True):

@@ -453,7 +453,6 @@ int or_solve_soa(float T[16], const float K[9], int rows, int cols, const float*
   return rounds;
 }
 
-/* P = K * (T_cw^-1)(0:3, 0:4), src/cam.cpp:109-112 ; row-major 3x4 out */
 /* or_solve_soa over the chunked-reduction linearize (timing only, see or_linearize_soa_mt). */
 int or_solve_soa_mt(float T[16], const float K[9], int rows, int cols, const float* x,
                     const float* y, const float* z, const float* u, const float* v, int64_t m,
@@ -481,6 +480,7 @@ int or_solve_soa_mt(float T[16], const float K[9], int rows, int cols, const flo
   return rounds;
 }
 
+/* P = K * (T_cw^-1)(0:3, 0:4), src/cam.cpp:109-112 ; row-major 3x4 out */
 void or_projection_matrix(const float K[9], const float T_cw[16], float P[12]) {
   float Ti[16];
   or_iso_inverse(T_cw, Ti);
@@ -566,6 +566,32 @@ void or_triangulate(const float P1[12], const float P2[12], const float* uv1, co
     xyz_out[3 * i + 1] = X4[1] * scale;
     xyz_out[3 * i + 2] = X4[2] * scale;
   }
+}
+
+/* One point of cv::triangulatePoints in double (recoverPose's use, normalised coordinates):
+ * the homogeneous DLT solution X4 (unnormalised, sign arbitrary). */
+void or_triangulate_h(const double P1[12], const double P2[12], const double* a, const double* b,
+                      double X4[4]) {
+  long double A[4][4];
+  const double* Ps[2] = {P1, P2};
+  const double* pts[2] = {a, b};
+  for (int j = 0; j < 2; ++j) {
+    const double x = pts[j][0], y = pts[j][1];
+    for (int k = 0; k < 4; ++k) {
+      A[2 * j + 0][k] = (long double)(x * Ps[j][8 + k] - Ps[j][0 + k]);
+      A[2 * j + 1][k] = (long double)(y * Ps[j][8 + k] - Ps[j][4 + k]);
+    }
+  }
+  long double S[4][4];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      long double s = 0.0L;
+      for (int k = 0; k < 4; ++k) s += A[k][r] * A[k][c];
+      S[r][c] = s;
+    }
+  long double v[4];
+  sym4_min_eigvec(S, v);
+  for (int k = 0; k < 4; ++k) X4[k] = (double)v[k];
 }
 
 /* match_points, src/my_utilities.h:70-120 (see picp_oracle.h) */

@@ -151,6 +151,32 @@ int64_t or_vo_segment(const float K[9], int rows, int cols, const int64_t* frame
 /* Eigen::Isometry3f::inverse() (rigid inverse) */
 void or_iso_inverse(const float T[16], float Tinv[16]);
 
+
+/* ---- essential-matrix bootstrap (picp_essential.c; src/cam.cpp:37-91) ----
+ * Nister's five-point solver: q1, q2 = five normalised points (x, y pairs), Es = up to 10
+ * row-major 3x3 essential matrices (unit Frobenius norm) with q2^T E q1 = 0; returns the count. */
+int or_five_point(const double* q1, const double* q2, double* Es);
+/* the RANSAC subsets of OpenCV's RANSACPointSetRegistrator (its cv::RNG((uint64)-1) stream):
+ * 5 * max_iters indices into n points */
+int or_essential_samples(int n, int max_iters, int* idx);
+/* RANSACUpdateNumIters */
+int or_ransac_update_iters(double p, double ep, int model_points, int max_iters);
+/* cv::findEssentialMat(p1, p2, K, RANSAC, prob, threshold, maxIters): p1/p2 = n float pixel
+ * (x, y) pairs, K = {fx, fy, cx, cy}, q_scratch = 4n doubles, idx_scratch = 5 * max_iters ints.
+ * Returns the inlier count of the best E (written row-major); 0 = no model. */
+int or_find_essential(const float* p1, const float* p2, int n, const double K[4], double prob,
+                      double threshold, int max_iters, double* q_scratch, int* idx_scratch,
+                      double E_out[9]);
+/* cv::decomposeEssentialMat */
+void or_decompose_essential(const double* E, double R1[9], double R2[9], double t[3]);
+/* cv::recoverPose(E, p1, p2, K, R, t, distanceThresh, mask): R row-major, t unit; mask (n bytes,
+ * may be NULL) marks the points in front of both cameras; returns their count */
+int or_recover_pose(const double E[9], const float* p1, const float* p2, int n, const double K[4],
+                    double dist, double* q_scratch, double R_out[9], double t_out[3], uint8_t* mask);
+/* one point of cv::triangulatePoints in double: homogeneous X4 (unnormalised) */
+void or_triangulate_h(const double P1[12], const double P2[12], const double* a, const double* b,
+                      double X4[4]);
+
 #ifdef __cplusplus
 }
 #endif

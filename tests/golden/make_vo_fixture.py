@@ -63,8 +63,13 @@ def main():
     # distinct landmarks the run triangulated (490, README:7).  Only the ids are kept: the
     # coordinates depend on the RANSAC bootstrap and the umeyama scale.
     wp = np.loadtxt(os.path.join(REF, "output", "estimated_world_points.txt"), dtype=np.float64)
+    # the reference's estimated trajectory (output/estimated_trajectory.txt, exec/icp_test.cpp:
+    # 181-182: frame, x, y, heading of cameraToImage * pose): its row 1 is the bootstrap of
+    # computeEssentialAndRecoverPose (src/cam.cpp:37-91) after frame 1's PICP
+    traj = np.loadtxt(os.path.join(REF, "output", "estimated_trajectory.txt"), dtype=np.float64)
     np.savez_compressed(
         OUT, ref_errors=errs.astype(np.float32), ref_map_ids=wp[:, 0].astype(np.int32),
+        ref_trajectory=traj,
         world_id=np.array(wid, np.int32), world_xyz=np.array(wxyz, np.float32),
         world_desc=np.array(wdesc, np.float32),
         gt_pose=gt, odom_pose=odom,
