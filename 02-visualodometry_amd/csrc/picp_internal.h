@@ -76,6 +76,17 @@ struct MatchProblem {
 };
 
 // ---------------------------------------------------------------------------------------
+// essential-matrix bootstrap (picp_essential.hip; src/cam.cpp:37-91), by value
+struct EssArgs {
+  int32_t n_problems;
+  int32_t max_iters;   // findEssentialMat maxIters (RANSAC hypotheses scored per problem)
+  double fx, fy, cx, cy;
+  double prob;         // findEssentialMat prob
+  double threshold;    // findEssentialMat threshold (pixels)
+  double dist;         // recoverPose distanceThresh
+};
+
+// ---------------------------------------------------------------------------------------
 // device-resident VO sequence (picp_vo.hip): exec/icp_test.cpp:36-136 per segment
 struct VoSegment {
   int64_t f0;       // first frame of the segment (bootstrap pair = f0, f0+1)

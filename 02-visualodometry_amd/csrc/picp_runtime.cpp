@@ -58,6 +58,10 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              float* second_dist, int32_t* accepted);
 extern "C" int picp_match_prep_kch(int dim);
 extern "C" __global__ void picp_rcp_check_kernel(int e_lo, int e_hi, unsigned long long* bad);
+extern "C" hipError_t picp_launch_essential(hipStream_t stream, const EssArgs* args, const int64_t* offs,
+                                           const float* p1, const float* p2, int32_t* idx, double* Es,
+                                           int32_t* ns, int32_t* cnt, float* T_out, int32_t* inliers,
+                                           int32_t* good, uint8_t* mask);
 extern "C" hipError_t picp_launch_gather(hipStream_t stream, const float* world,
                                          const float* image, const int2* pairs, int64_t m,
                                          float* X, float* Y, float* Z, float* U, float* V,
@@ -1089,6 +1093,98 @@ extern "C" int picp_triangulate(int device, const float P1[12], const float P2[1
   if (e == hipSuccess) e = hipMemcpy(xyz, dxyz, (size_t)q * 3 * sizeof(float), hipMemcpyDeviceToHost);
   hipFree(buf);
   if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_triangulate: %s", hipGetErrorString(e));
+  return PICP_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// essential-matrix bootstrap (src/cam.cpp:37-91: findEssentialMat + recoverPose)
+// ------------------------------------------------------------------------------------
+extern "C" void picp_essential_params_default(picp_essential_params* p) {
+  if (!p) return;
+  p->prob = 0.999;       // cv::findEssentialMat defaults (src/cam.cpp:49-54 passes none)
+  p->threshold = 1.0;
+  p->max_iters = 1000;
+  p->dist = 50.0;        // cv::recoverPose distanceThresh default
+}
+
+extern "C" int picp_essential_batch(int device, int n_problems, const int64_t* offs, const float* p1,
+                                    const float* p2, const float K[9], const picp_essential_params* prm,
+                                    float* T_out, int32_t* inliers, int32_t* good, uint8_t* mask) {
+  CHECK_ARG(n_problems >= 1 && offs && K && T_out && inliers && good, "picp_essential_batch: null argument");
+  CHECK_ARG(offs[0] == 0, "picp_essential_batch: offsets must start at 0");
+  for (int i = 0; i < n_problems; ++i)
+    CHECK_ARG(offs[i + 1] >= offs[i] && offs[i + 1] - offs[i] <= INT32_MAX, "picp_essential_batch: bad offsets");
+  const int64_t total = offs[n_problems];
+  CHECK_ARG(total == 0 || (p1 && p2), "picp_essential_batch: null points");
+  picp_essential_params dp;
+  picp_essential_params_default(&dp);
+  const picp_essential_params& P = prm ? *prm : dp;
+  CHECK_ARG(P.max_iters >= 1 && P.max_iters <= 100000, "picp_essential_batch: max_iters out of range");
+  CHECK_ARG(P.threshold > 0.0 && P.prob > 0.0 && P.prob < 1.0 && P.dist > 0.0, "picp_essential_batch: bad params");
+  CHECK_ARG(K[0] != 0.0f && K[4] != 0.0f, "picp_essential_batch: K has a zero focal length");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  CHECK_ARG(device >= 0 && device < ndev, "picp_essential_batch: no such HIP device");
+  HIP_TRY(hipSetDevice(device));
+  EssArgs A;
+  memset(&A, 0, sizeof(A));
+  A.n_problems = n_problems;
+  A.max_iters = P.max_iters;
+  A.fx = K[0];  // column-major 3x3 (src/camera.h:45): K(0,0), K(1,1), K(0,2), K(1,2)
+  A.fy = K[4];
+  A.cx = K[6];
+  A.cy = K[7];
+  A.prob = P.prob;
+  A.threshold = P.threshold;
+  A.dist = P.dist;
+  const size_t H = (size_t)n_problems * P.max_iters;
+  const size_t pts = (size_t)std::max<int64_t>(total, 1) * 2 * sizeof(float);
+  // one allocation carved into 256-byte-aligned sub-buffers (sizes rounded the same way)
+  auto r256 = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t bytes = r256((size_t)(n_problems + 1) * 8) + 2 * r256(pts) + r256(H * 5 * 4) + r256(H * 90 * 8) +
+                       r256(H * 4) + r256(H * 10 * 4) + r256((size_t)n_problems * 16 * 4) +
+                       2 * r256((size_t)n_problems * 4) + r256((size_t)std::max<int64_t>(total, 1));
+  char* buf = nullptr;
+  HIP_TRY(hipMalloc(&buf, bytes));
+  size_t at = 0;
+  auto carve = [&](size_t b) { char* q = buf + at; at += r256(b); return q; };
+  int64_t* d_offs = (int64_t*)carve((size_t)(n_problems + 1) * 8);
+  float* d_p1 = (float*)carve(pts);
+  float* d_p2 = (float*)carve(pts);
+  int32_t* d_idx = (int32_t*)carve(H * 5 * 4);
+  double* d_Es = (double*)carve(H * 90 * 8);
+  int32_t* d_ns = (int32_t*)carve(H * 4);
+  int32_t* d_cnt = (int32_t*)carve(H * 10 * 4);
+  float* d_T = (float*)carve((size_t)n_problems * 16 * 4);
+  int32_t* d_in = (int32_t*)carve((size_t)n_problems * 4);
+  int32_t* d_good = (int32_t*)carve((size_t)n_problems * 4);
+  uint8_t* d_mask = mask ? (uint8_t*)carve((size_t)std::max<int64_t>(total, 1)) : nullptr;
+  hipError_t e = hipMemcpy(d_offs, offs, (size_t)(n_problems + 1) * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess && total > 0) e = hipMemcpy(d_p1, p1, (size_t)total * 2 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && total > 0) e = hipMemcpy(d_p2, p2, (size_t)total * 2 * sizeof(float), hipMemcpyHostToDevice);
+  const char* stage = "upload";
+  if (e == hipSuccess) {
+    stage = "launch";
+    e = picp_launch_essential(nullptr, &A, d_offs, d_p1, d_p2, d_idx, d_Es, d_ns, d_cnt, d_T, d_in, d_good, d_mask);
+  }
+  if (e == hipSuccess) {
+    stage = "download T";
+    e = hipMemcpy(T_out, d_T, (size_t)n_problems * 16 * 4, hipMemcpyDeviceToHost);
+  }
+  if (e == hipSuccess) {
+    stage = "download inliers";
+    e = hipMemcpy(inliers, d_in, (size_t)n_problems * 4, hipMemcpyDeviceToHost);
+  }
+  if (e == hipSuccess) {
+    stage = "download good";
+    e = hipMemcpy(good, d_good, (size_t)n_problems * 4, hipMemcpyDeviceToHost);
+  }
+  if (e == hipSuccess && mask && total > 0) {
+    stage = "download mask";
+    e = hipMemcpy(mask, d_mask, (size_t)total, hipMemcpyDeviceToHost);
+  }
+  hipFree(buf);
+  if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_essential_batch (%s): %s", stage, hipGetErrorString(e));
   return PICP_OK;
 }
 

@@ -43,7 +43,7 @@ EXPORTED = [
     "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
     "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async",
     "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
-    "picp_vo_info", "picp_selftest_rcp",
+    "picp_vo_info", "picp_selftest_rcp", "picp_essential_params_default", "picp_essential_batch",
 ]
 
 
@@ -417,6 +417,44 @@ def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, devi
     return [{"best_idx": bi[o1[i]:o1[i + 1]], "best_dist": bd[o1[i]:o1[i + 1]],
              "second_dist": sd[o1[i]:o1[i + 1]], "accepted": acc[o1[i]:o1[i + 1]].astype(bool)}
             for i in range(len(desc1_list))]
+
+
+class EssentialParams(ctypes.Structure):
+    """picp_essential_params (include/picp_c.h): cv::findEssentialMat / cv::recoverPose knobs."""
+    _fields_ = [("prob", ctypes.c_double), ("threshold", ctypes.c_double), ("max_iters", ctypes.c_int),
+                ("reserved", ctypes.c_int), ("dist", ctypes.c_double)]
+
+
+def essential_recover_pose_batch(p1_list, p2_list, K=None, prob=0.999, threshold=1.0, max_iters=1000,
+                                 dist=50.0, device=0, want_mask=False):
+    """Cam::computeEssentialAndRecoverPose (src/cam.cpp:37-91) on the GPU for many two-view
+    problems: findEssentialMat(RANSAC) + recoverPose.  Returns per problem a dict with T (4x4
+    camera-in-world of the second view, the first at the origin, unit baseline), inliers, good
+    (and mask)."""
+    K = K_REF if K is None else K
+    offs = np.zeros(len(p1_list) + 1, np.int64)
+    offs[1:] = np.cumsum([len(p) for p in p1_list])
+    n = int(offs[-1])
+    p1 = np.ascontiguousarray(np.concatenate([np.asarray(p, np.float32).reshape(-1, 2) for p in p1_list])
+                              if n else np.zeros((0, 2), np.float32))
+    p2 = np.ascontiguousarray(np.concatenate([np.asarray(p, np.float32).reshape(-1, 2) for p in p2_list])
+                              if n else np.zeros((0, 2), np.float32))
+    prm = EssentialParams(prob, threshold, max_iters, 0, dist)
+    T = np.zeros(16 * len(p1_list), np.float32)
+    inl = np.zeros(len(p1_list), np.int32)
+    good = np.zeros(len(p1_list), np.int32)
+    mask = np.zeros(max(n, 1), np.uint8) if want_mask else None
+    _check(lib().picp_essential_batch(device, len(p1_list), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                      _fptr(p1) if n else None, _fptr(p2) if n else None, _fptr(k_to_c(K)),
+                                      ctypes.byref(prm), _fptr(T), _i32ptr(inl), _i32ptr(good),
+                                      mask.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if want_mask else None))
+    out = []
+    for i in range(len(p1_list)):
+        d = {"T": pose_from_c(T[16 * i:16 * i + 16]), "inliers": int(inl[i]), "good": int(good[i])}
+        if want_mask:
+            d["mask"] = mask[offs[i]:offs[i + 1]].astype(bool)
+        out.append(d)
+    return out
 
 
 class VOSequence:

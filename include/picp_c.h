@@ -175,6 +175,32 @@ int picp_match_batch(int device, int n_problems, const int64_t* off1, const int6
                      float ratio_thr, int32_t* best_idx, float* best_dist, float* second_dist,
                      int32_t* accepted);
 
+/* ---------------- essential-matrix bootstrap (src/cam.cpp:37-91) ---------------- */
+
+/* Cam::computeEssentialAndRecoverPose: cv::findEssentialMat(p1, p2, K, cv::RANSAC) then
+ * cv::recoverPose(E, p1, p2, K, R, t, mask), for many independent two-view problems.  The RANSAC
+ * subsets are OpenCV's (its RNG((uint64)-1) stream), the minimal solver is Nister's five-point
+ * algorithm, and the selection rule and adaptive iteration bound are OpenCV's. */
+typedef struct picp_essential_params {
+  double prob;       /* findEssentialMat prob      (default 0.999) */
+  double threshold;  /* findEssentialMat threshold (default 1.0 px) */
+  int max_iters;     /* findEssentialMat maxIters  (default 1000) */
+  int reserved;
+  double dist;       /* recoverPose distanceThresh (default 50) */
+} picp_essential_params;
+
+void picp_essential_params_default(picp_essential_params* p);
+
+/* Problem i: the pixel pairs (p1[k], p2[k]) for k in [offs[i], offs[i+1]) (float x, y each).
+ * K: column-major 3x3.  prm may be NULL (defaults).  Out, per problem: T_out[16 i ..] = the
+ * camera-in-world pose of the second view with the first at the origin, [R | t]^-1 column-major
+ * (Cam::getPose, src/cam.cpp:81,227; unit baseline), inliers = findEssentialMat's inlier count
+ * (0: no model, T = I), good = recoverPose's count.  mask (may be NULL): offs[n] bytes, 1 for
+ * the points recoverPose keeps. */
+int picp_essential_batch(int device, int n_problems, const int64_t* offs, const float* p1,
+                         const float* p2, const float K[9], const picp_essential_params* prm,
+                         float* T_out, int32_t* inliers, int32_t* good, uint8_t* mask);
+
 /* ---------------- device-resident VO sequence (exec/icp_test.cpp:36-136) ---------------- */
 
 /* The reference's per-frame loop (match next<->map, PICP from the previous pose, match
