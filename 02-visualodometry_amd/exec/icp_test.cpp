@@ -1,7 +1,8 @@
 // icp_test -- the reference's published pipeline (exec/icp_test.cpp:17-215) driven through the
 // drop-in pr:: facade, i.e. on the MI355X PICP + triangulation kernels.
 //
-//   icp_test [data_dir=./data] [out_dir=./output] [--fused | --vo] [--frames N] [--device D]
+//   icp_test [data_dir=./data] [out_dir=./output] [--fused | --vo] [--gt-bootstrap] [--frames N]
+//            [--device D]
 //
 // Per frame, as the reference: match the next frame's descriptors to the map
 // (match_points, src/my_utilities.h:70-120), PICP from the previous pose (threshold 3000, <= 50
@@ -10,9 +11,9 @@
 // between the previous and the new pose (src/cam.cpp:94-140).  Then scale-align the trajectory
 // (Umeyama scale, src/my_utilities.cpp:459-478) and write output/*.txt like the reference.
 //
-// Documented stand-ins: the bootstrap pose of frame 1 comes from the ground-truth relative pose
-// normalised to unit translation -- what cv::findEssentialMat + cv::recoverPose
-// (src/cam.cpp:37-91, OpenCV RANSAC, out of scope) return for noise-free matches.  --fused runs
+// The bootstrap pose of frame 1 is cv::findEssentialMat(RANSAC) + cv::recoverPose
+// (src/cam.cpp:37-91) on the GPU (picp_essential_batch, OpenCV's RANSAC subsets replayed);
+// --gt-bootstrap substitutes the ground-truth relative pose normalised to unit translation.  --fused runs
 // the icp loop as one device solve (pr::PICPSolver::solve) instead of host-driven oneRound().
 // Descriptor matching runs on the GPU matcher (picp_match).  --vo runs the whole per-frame loop
 // device-resident (picp_vo_*: match, PICP, match, select, triangulate, append on the GPU) and
@@ -205,12 +206,13 @@ double umeyama_scale(const std::vector<pr::Vector3f>& P, const std::vector<pr::V
 
 int main(int argc, char** argv) {
   std::string data_dir = "./data", out_dir = "./output";
-  bool fused = false, vo = false;
+  bool fused = false, vo = false, gt_bootstrap = false;
   int n_meas = 121, device = 0, pos = 0;
   for (int a = 1; a < argc; ++a) {
     std::string s = argv[a];
     if (s == "--fused") fused = true;
     else if (s == "--vo") vo = true;
+    else if (s == "--gt-bootstrap") gt_bootstrap = true;
     else if (s == "--frames" && a + 1 < argc) n_meas = std::atoi(argv[++a]);
     else if (s == "--device" && a + 1 < argc) device = std::atoi(argv[++a]);
     else if (pos == 0) { data_dir = s; ++pos; }
@@ -256,14 +258,41 @@ int main(int argc, char** argv) {
     }
   };
 
-  // bootstrap (stand-in for computeEssentialAndRecoverPose, see header)
+  // bootstrap: Cam::computeEssentialAndRecoverPose on the matches of frames 0-1
+  // (exec/icp_test.cpp:44-51, src/cam.cpp:37-91) -> picp_essential_batch; the pose of frame 1 is
+  // Cam::getPose = [R | t]^-1 (unit baseline).  --gt-bootstrap: the gt relative pose normalised
+  // to unit translation instead.
   pr::IntPairVector init_corr;
   match_points(meas[0].points, meas[1].points, init_corr);
-  const pr::Isometry3f M = camera_mount();
-  pr::Isometry3f T01 = (planar_pose(meas[0].gt) * M).inverse() * (planar_pose(meas[1].gt) * M);
-  pr::Vector3f t01 = T01.translation();
-  const float tn = t01.norm();
-  T01(0, 3) = t01[0] / tn; T01(1, 3) = t01[1] / tn; T01(2, 3) = t01[2] / tn;
+  pr::Isometry3f T01 = pr::Isometry3f::Identity();
+  if (gt_bootstrap) {
+    const pr::Isometry3f M = camera_mount();
+    T01 = (planar_pose(meas[0].gt) * M).inverse() * (planar_pose(meas[1].gt) * M);
+    pr::Vector3f t01 = T01.translation();
+    const float tn = t01.norm();
+    T01(0, 3) = t01[0] / tn; T01(1, 3) = t01[1] / tn; T01(2, 3) = t01[2] / tn;
+  } else {
+    std::vector<float> p1, p2;
+    for (auto& c : init_corr) {
+      p1.push_back(meas[0].points[c.first].u);
+      p1.push_back(meas[0].points[c.first].v);
+      p2.push_back(meas[1].points[c.second].u);
+      p2.push_back(meas[1].points[c.second].v);
+    }
+    const int64_t offs[2] = {0, (int64_t)init_corr.size()};
+    float T16[16];
+    int32_t inliers = 0, good = 0;
+    if (picp_essential_batch(device, 1, offs, p1.data(), p2.data(), pr::data9(K), nullptr, T16, &inliers,
+                             &good, nullptr) != PICP_OK) {
+      std::cerr << "essential bootstrap failed: " << picp_last_error() << std::endl;
+      return EXIT_FAILURE;
+    }
+    if (inliers == 0) {  // src/cam.cpp:58-61
+      std::cerr << "Essential matrix computation failed!" << std::endl;
+      return EXIT_FAILURE;
+    }
+    T01 = pr::iso_from16(T16);
+  }
   long total_rounds = 0;
   double picp_ms = 0;
   if (vo) {
@@ -426,8 +455,9 @@ int main(int argc, char** argv) {
   const double n = (double)poses.size();
   std::printf("{\"frames\": %d, \"world_points\": %zu, \"scale\": %.6f, \"trans_err_mean\": %.6f, "
               "\"trans_err_rmse\": %.6f, \"trans_err_max\": %.6f, \"yaw_err_wrapped_mean\": %.6f, "
-              "\"yaw_err_wrapped_max\": %.6f, \"picp_rounds\": %ld, \"picp_ms\": %.3f, \"fused\": %d, \"vo\": %d}\n",
+              "\"yaw_err_wrapped_max\": %.6f, \"picp_rounds\": %ld, \"picp_ms\": %.3f, \"fused\": %d, \"vo\": %d, "
+              "\"bootstrap\": \"%s\"}\n",
               (int)n, world.size(), scale, sum_e / n, std::sqrt(sum_e2 / n), max_e, sum_yaw / n, max_yaw,
-              total_rounds, picp_ms, fused ? 1 : 0, vo ? 1 : 0);
+              total_rounds, picp_ms, fused ? 1 : 0, vo ? 1 : 0, gt_bootstrap ? "gt" : "essential");
   return 0;
 }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # full GPU pass: tests, smoke, bench, rocprof kernel stats (each step time-limited; stop on failure)
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -6 gpurun_out/pytest_gpu.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
