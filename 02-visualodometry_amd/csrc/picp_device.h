@@ -638,10 +638,23 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
   for (int i = 0; i < 3; ++i) t[i] = tn[i];
 }
 
-// Finish round (j-1) of a problem from its block-partial totals: H, b, stats -> new state.
-// Runs in one lane; everything is indexed by compile-time constants.
-__device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState& s,
-                                             const double* tot, int j, PicpState& ns) {
+// The 32 block-partial totals (double) -> the float words finish_round_f consumes, one word per
+// total so lane e of a wave can convert total e: H entries with the damping added on the
+// diagonal (src/picp_solver.cpp:96), -b, chi_in, chi_out as float, n_in and n_proj as int bits.
+__device__ __forceinline__ float total_word(const PicpArgs& A, int e, double t) {
+  const bool diag = (e == 0) | (e == 6) | (e == 11) | (e == 15) | (e == 18) | (e == 20);
+  if (e < PICP_P_B) return (float)(t + (diag ? (double)A.damping : 0.0));
+  if (e < PICP_P_CHI_IN) return (float)(-t);
+  if (e < PICP_P_N_IN) return (float)t;
+  if (e < 31) return __int_as_float((int32_t)t);
+  return 0.0f;
+}
+
+// Finish round (j-1) of a problem from its converted totals (total_word): damping is already
+// in, so this is the min-inlier check, the 6x6 solve, the update and the icp_test loop state.
+// Runs in one lane (or redundantly in several); everything is indexed by compile-time constants.
+__device__ __forceinline__ void finish_round_f(const PicpArgs& A, const PicpState& s,
+                                               const float* tw, int j, PicpState& ns) {
   // field-wise, padding zeroed: a whole-struct copy of an LDS state kept its 44-byte tail in a
   // scratch alloca (SROA cannot split the memcpy), a round trip on every round's critical path
 #pragma unroll
@@ -654,10 +667,10 @@ __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState&
   ns.converged = s.converged;
 #pragma unroll
   for (int i = 0; i < 11; ++i) ns.pad[i] = 0;
-  ns.chi_in = (float)tot[PICP_P_CHI_IN];
-  ns.chi_out = (float)tot[PICP_P_CHI_OUT];
-  ns.n_in = (int32_t)tot[PICP_P_N_IN];
-  ns.n_proj = (int32_t)tot[PICP_P_N_PROJ];
+  ns.chi_in = tw[PICP_P_CHI_IN];
+  ns.chi_out = tw[PICP_P_CHI_OUT];
+  ns.n_in = __float_as_int(tw[PICP_P_N_IN]);
+  ns.n_proj = __float_as_int(tw[PICP_P_N_PROJ]);
   ns.rounds = j;
   float H[6][6];
   int k = 0;
@@ -665,9 +678,8 @@ __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState&
   for (int r = 0; r < 6; ++r)
 #pragma unroll
     for (int c = r; c < 6; ++c) {
-      const double h = tot[PICP_P_H + k] + ((r == c) ? (double)A.damping : 0.0);  // :96
-      H[r][c] = (float)h;
-      H[c][r] = (float)h;
+      H[r][c] = tw[PICP_P_H + k];  // :96 (damping folded in by total_word)
+      H[c][r] = tw[PICP_P_H + k];
       ++k;
     }
   if (ns.n_in < A.min_inliers) {  // src/picp_solver.cpp:97-100
@@ -677,7 +689,7 @@ __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState&
   }
   float nb[6], dx[6];
 #pragma unroll
-  for (int r = 0; r < 6; ++r) nb[r] = (float)(-tot[PICP_P_B + r]);
+  for (int r = 0; r < 6; ++r) nb[r] = tw[PICP_P_B + r];
   ldlt6_solve(H, nb, dx);        // :102
   apply_update(dx, ns.R, ns.t);  // :103
   ns.ok = 1;
@@ -691,6 +703,16 @@ __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState&
     ns.chi_prev = cur;
   }
   if (j >= A.max_rounds) ns.done = 1;
+}
+
+// Finish round (j-1) of a problem from its block-partial totals (double): H, b, stats -> new
+// state.  One lane.
+__device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState& s,
+                                             const double* tot, int j, PicpState& ns) {
+  float tw[PICP_NPART];
+#pragma unroll
+  for (int e = 0; e < PICP_NPART; ++e) tw[e] = total_word(A, e, tot[e]);
+  finish_round_f(A, s, tw, j, ns);
 }
 
 

@@ -27,6 +27,10 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #define PICP_MAX_PBLK 256   // max blocks per problem in this mode (sweep registers)
 #define PICP_PBLOCK 512     // threads per block: 8 waves, 2 per SIMD (<= 256 VGPRs)
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
+// raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
+// never hoisted out of a spin loop)
+#define PICP_AUX_SC1_VOLATILE ((int)(16u | 0x80000000u))
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Diagnostic build only (-DPICP_STAMPS): s_memrealtime per phase of rounds (epochs) 11 and 12.
 #ifdef PICP_STAMPS
@@ -58,8 +62,8 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
     unsigned long long* gpart, unsigned long long* gpose, unsigned int* err,
     unsigned long long timeout_ticks) {
-  __shared__ double s_red[PICP_PBLOCK / 32][PICP_NPART + 1];
-  __shared__ double s_tot[PICP_NPART];
+  __shared__ double s_red[PICP_PBLOCK / 64][PICP_NPART + 1];
+  __shared__ float s_tot[PICP_NPART];
   __shared__ float s_wave[PICP_PBLOCK / 64][PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
@@ -174,17 +178,20 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     PSTAMP(1);
 
     if (leader) {
-      // ---- 2. sweep the problem's partials (entry e = tid&31 of blocks (tid>>5) + 8i) ----
-      const int e = tid & 31, g = tid >> 5;
-      constexpr int NG = PICP_PBLOCK / 32;  // block groups swept in parallel
+      // ---- 2. sweep the problem's partials: 16-B sc1 loads of granule pairs (2c, 2c+1) of
+      //         blocks g + NG*i (c = tid&15, g = tid>>4); each 8-B half carries its own tag ----
+      const int c = tid & 15, g = tid >> 4;
+      constexpr int NG = PICP_PBLOCK / 16;  // block groups swept in parallel
       constexpr int MAXG = PICP_MAX_PBLK / NG;
-      unsigned long long gv[MAXG];
-      // re-poll only the granules whose tag has not matched yet: a full 50 KB sweep costs
-      // ~0.8 us at one block's share of the fabric, a re-poll of the few late blocks far less
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(prob_part0 + (epoch & 1) * part_stride), 0, nblk * PICP_NPART * 8, 0x00020000);
+      u32x4 gv[MAXG];
+      // re-poll only the pairs whose tags have not both matched yet: a full 50 KB sweep costs
+      // ~0.5 us at one block's share of the fabric, a re-poll of the few late blocks far less
       unsigned pending = 0;
 #pragma unroll
       for (int i = 0; i < MAXG; ++i) {
-        gv[i] = 0;
+        gv[i] = (u32x4){0u, 0u, 0u, 0u};
         if (g + NG * i < nblk) pending |= 1u << i;
       }
       for (;;) {
@@ -192,10 +199,11 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
 #pragma unroll
         for (int i = 0; i < MAXG; ++i)
           if (want & (1u << i))
-            gv[i] = __hip_atomic_load(prob_part0 + (epoch & 1) * part_stride + (size_t)(g + NG * i) * PICP_NPART + e, RLX_AGENT);
+            gv[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((g + NG * i) * PICP_NPART + 2 * c) * 8, 0,
+                                                           PICP_AUX_SC1_VOLATILE);
 #pragma unroll
         for (int i = 0; i < MAXG; ++i)
-          if ((want & (1u << i)) && (unsigned)(gv[i] >> 32) == epoch) pending &= ~(1u << i);
+          if ((want & (1u << i)) && gv[i][1] == epoch && gv[i][3] == epoch) pending &= ~(1u << i);
         if (!pending) break;
         if (timed_out(deadline)) {
           __hip_atomic_store(errw, 1u, RLX_AGENT);
@@ -203,44 +211,67 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      double acc = 0.0;
+      double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
       for (int i = 0; i < MAXG; ++i)
-        if (g + NG * i < nblk) acc += (double)__uint_as_float((unsigned)gv[i]);
-      s_red[g][e] = acc;
-      __syncthreads();
-      PSTAMP(2);
-      if (tid < PICP_NPART) {
-        double t = 0.0;
-#pragma unroll
-        for (int gg = 0; gg < NG; ++gg) t += s_red[gg][tid];
-        s_tot[tid] = t;
+        if (g + NG * i < nblk) {
+          acc0 += (double)__uint_as_float(gv[i][0]);
+          acc1 += (double)__uint_as_float(gv[i][2]);
+        }
+      // the wave's four groups (lanes c, 16+c, 32+c, 48+c) first: every lane ends with the same
+      // (a0+a1)+(a2+a3) (IEEE addition commutes), so the order stays fixed
+      acc0 += __shfl_xor(acc0, 16);
+      acc1 += __shfl_xor(acc1, 16);
+      acc0 += __shfl_xor(acc0, 32);
+      acc1 += __shfl_xor(acc1, 32);
+      if (lane < 16) {
+        s_red[wave][2 * c] = acc0;
+        s_red[wave][2 * c + 1] = acc1;
       }
       __syncthreads();
-      if (tid == 0) {
-        double tot[PICP_NPART];
+      PSTAMP(2);
+      // ---- finish the round in wave 0 only: lanes < 32 combine the groups (fixed order), then
+      //      lanes 0-15 all run the solve (uniform work, one lane's latency) and each publishes
+      //      its pose word directly; the other waves meet wave 0 at the barrier below, off the
+      //      publish path ----
+      if (wave == 0) {
+        if (lane < PICP_NPART) {
+          double t = 0.0;
 #pragma unroll
-        for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
-        PicpState ns;
-        PSTAMP(4);
-        finish_round(A, s_st, tot, (int)epoch, ns);
-        PSTAMP(5);
-        if (__hip_atomic_load(errw, RLX_AGENT) != 0u) ns.done = 1;  // a sweep timed out
-        s_st = ns;
+          for (int w = 0; w < PICP_PBLOCK / 64; ++w) t += s_red[w][lane];
+          s_tot[lane] = total_word(A, lane, t);  // lane e converts total e
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < PICP_POSE_GRAN) {
+          float tw[PICP_NPART];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
+          for (int i = 0; i < PICP_NPART; ++i) tw[i] = s_tot[i];
+          PicpState ns;
+          PSTAMP(4);
+          finish_round_f(A, s_st, tw, (int)epoch, ns);
+          PSTAMP(5);
+          if (__hip_atomic_load(errw, RLX_AGENT) != 0u) ns.done = 1;  // a sweep timed out
+          // ---- publish the new pose (and the done flag): lane l owns word l ----
+          float w = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
-        s_done = ns.done;
-        if (ns.done && leader) st_out[p] = ns;
+          for (int i = 0; i < 9; ++i) w = (lane == i) ? ns.R[i] : w;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) w = (lane == 9 + i) ? ns.t[i] : w;
+          w = (lane == 12) ? __int_as_float(ns.done) : w;
+          __hip_atomic_store(prob_pose + lane, granule(epoch, w), RLX_AGENT);
+          if (lane == 0) {
+            s_st = ns;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
+            s_done = ns.done;
+            if (ns.done) st_out[p] = ns;
+          }
+        }
       }
       __syncthreads();
       PSTAMP(3);
-      // ---- publish the new pose (and the done flag) ----
-      if (tid < PICP_POSE_GRAN) {
-        const float w = (tid < 12) ? s_pose[tid] : ((tid == 12) ? __int_as_float(s_done) : 0.0f);
-        __hip_atomic_store(prob_pose + tid, granule(epoch, w), RLX_AGENT);
-      }
     } else {
       // ---- 3. wait for the leader's pose of this round (one wave, 16 lanes) ----
       if (wave == 0) {
