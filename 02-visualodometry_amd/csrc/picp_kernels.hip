@@ -116,6 +116,15 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
 
   const int tid = threadIdx.x;
   STAMP(0);
+#ifdef PICP_STAMPS
+  if (threadIdx.x == 0 && (j == 10 || j == 11) && blockIdx.x < PICP_STAMP_BLOCKS) {
+    unsigned xcc, hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    picp_stamps[j - 10][blockIdx.x][6] = xcc;
+    picp_stamps[j - 10][blockIdx.x][7] = hwid;
+  }
+#endif
   int p, first = 0, count = 0, blk0, nblk;
   int64_t base;
   if (A.uniform) {

@@ -422,6 +422,28 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     }
     blk += nb;
   }
+  // Streaming single frame on two blocks per CU (nblk == 2 x CUs): the hardware issues the
+  // older block of a CU first, so with equal slices the first num_cu blocks finish a round at
+  // ~2/3 of the time the second ones need and their CUs then stream at half parallelism
+  // (tools/stamps_place.py).  Pair block q with q + num_cu over a contiguous
+  // range and give q the larger share (PICP_STREAM_SHARE, the first block's fraction).
+  if (b->mode == PICP_MODE_GRAPH && np == 1 && b->vec == 4 && nblk == 2 * b->num_cu) {
+    double share = 0.64;  // measured optimum (profiles/r01/sweep_share.log); 0.5 = equal slices
+    if (const char* e = getenv("PICP_STREAM_SHARE")) share = atof(e);
+    if (share > 0.5 && share < 0.9) {
+      const int64_t n = offs[1] - offs[0];
+      const int64_t pair = round_up((n + b->num_cu - 1) / b->num_cu, 4);
+      const int64_t hi = round_up((int64_t)(pair * share), 4);
+      for (int q = 0; q < b->num_cu; ++q) {
+        const int64_t f0 = std::min<int64_t>(n, q * pair);
+        const int64_t f1 = std::min<int64_t>(n, f0 + hi);
+        const int64_t f2 = std::min<int64_t>(n, (q + 1) * pair);
+        b->blk_h[q] = make_int4(0, (int)f0, (int)(f1 - f0), 0);
+        b->blk_h[q + b->num_cu] = make_int4(0, (int)f1, (int)(f2 - f1), 0);
+      }
+      b->uniform = 0;  // the kernel reads the block table
+    }
+  }
   HIP_TRY(hipMemcpyAsync(b->blk_d, b->blk_h.data(), (size_t)nblk * sizeof(int4), hipMemcpyHostToDevice, b->stream));
   // identity initial poses by default
   b->init_h.assign(np, PicpState{});

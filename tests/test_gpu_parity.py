@@ -461,6 +461,39 @@ def test_streaming_sweep_directions_ragged_tail(native, oracle, sizes):
             assert abs(stats[i]["n_in"] - st_ref["n_in"]) <= 2, (fwd, i)
 
 
+def test_streaming_weighted_pair_split_matches_oracle(native, oracle):
+    """A streaming single frame on two blocks per CU (>= 2^23 correspondences: 2 x CUs blocks)
+    gives each CU-pair's older block the larger share of a contiguous range (PICP_STREAM_SHARE,
+    DESIGN §4.1); equal shares (0.5) keep the uniform slices.  Both vs the oracle over a few
+    rounds (the oracle at this size takes ~0.5 s a round), replays bit-identical."""
+    import os
+    synth = _synth()
+    n = (1 << 23) + 4099  # ragged tail
+    p = synth.make_problem(n, seed=901, outlier_frac=0.2, pixel_noise=0.5, shuffle=False)
+    R = 3
+    res = {}
+    for share in ("0.5", "0.64"):
+        os.environ["PICP_STREAM_SHARE"] = share
+        try:
+            b = _batch_mode(native, [n], "graph")
+            info = b.info()
+            assert info["mode"] == "graph" and info["n_blocks"] % 2 == 0
+            b.set_data(p["xyz"], p["uv"])
+            b.set_poses(p["T_init"][None])
+            b.solve(threshold=THR, max_rounds=R, conv_eps=-1.0)
+            T, st = b.poses()[0], b.stats()[0]
+            b.solve(threshold=THR, max_rounds=R, conv_eps=-1.0)
+            np.testing.assert_array_equal(b.poses()[0], T)
+        finally:
+            os.environ.pop("PICP_STREAM_SHARE", None)
+        res[share] = (T, st)
+    T_ref, st_ref = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"], p["y"], p["z"], p["u"], p["v"],
+                                     THR, mode=oracle.MODE_F64, max_rounds=R, conv_eps=-1.0)
+    for share, (T, st) in res.items():
+        assert synth.se3_log_norm(T, T_ref) < POSE_TOL, share
+        assert abs(st["n_in"] - st_ref["n_in"]) <= 10, share
+
+
 @pytest.mark.parametrize("sizes", [[5000, 1, 3, 4097, 12000, 7], [10000] * 32])
 def test_block_split_matches_oracle(native, oracle, sizes):
     """Block mode with two blocks per problem (PICP_BLOCK_SPLIT=2, the C4 layout: halves on

@@ -15,11 +15,12 @@ os.environ["PICP_LIB"] = os.path.join(ROOT, "02-visualodometry_amd", "lib", "lib
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100000)
+    ap.add_argument("--outlier", type=float, default=0.0)
     args = ap.parse_args()
     import numpy as np
     import picp_amd
     from picp_amd import synth
-    p = synth.make_problem(args.n, seed=42, pixel_noise=0.5, shuffle=False)
+    p = synth.make_problem(args.n, seed=42, outlier_frac=args.outlier, pixel_noise=0.5, shuffle=False)
     b = picp_amd.Batch([args.n])
     info = b.info()
     assert info["mode"] == "persistent", info
