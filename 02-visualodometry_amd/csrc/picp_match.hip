@@ -229,7 +229,11 @@ __device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t)
   return m;
 }
 
-template <int KCH>
+// RAD = 1: the accept-only (radius) form for callers that consume only accepted[] and the
+// best_idx of accepted queries (the VO sequence): pass 1 is skipped and the candidates are the
+// references within a fixed radius of the query (mm_radius below); best_idx, best_dist and
+// second_dist are defined only where accepted[] is 1, accepted[] everywhere.
+template <int KCH, int RAD>
 __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
@@ -307,6 +311,34 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     for (int c = 0; c < KCH; ++c) bb[c] = s_t[b][col * (DP / 8) + 2 * c + hf];
   };
 
+  float tau[MM_RB][16];
+  float a1 = 0.0f;  // RAD: n2 is scaled by (1 - a1) before the compare (the per-pair bound)
+  int buf = 0;
+  if constexpr (RAD) {
+    // Accept-only (radius) candidates.  With R = (dist_thr / ratio_thr)(1 + 2^-10): a query the
+    // reference accepts has its best d* < dist_thr <= R, so every reference at d < R -- the
+    // best and, when it is < R, the second -- is a candidate, the index-order scan over them
+    // gives the reference's best index and best, and a second >= R gives best/second <
+    // ratio_thr/(1 + 2^-10), accepted either way; a rejected query (d* >= dist_thr) stays
+    // rejected because candidates are a subset.  The pass-1 error bound depends on the pair
+    // only through t = |q|^2 + |r|^2 (Rmax above only bounds |r|^2), E(t) = A t + B, so with
+    // twice its headroom (a1 = 2A, 2B) the test D' <= R - |q|^2 + 2E(t) is
+    //   fma(-2, q.r, n2 (1 - a1)) <= R - |q|^2 + a1 |q|^2 + 2B.
+    const float v = 1.0f / 2048.0f, u = 1.0f / 16777216.0f, bq = 1.0f / 4194304.0f;
+    a1 = 3.0f * ((2.0f * v + v * v + 56.0f * u) + bq);
+    const float b2 = 3.0f * bq;
+    const float R = (dist_thr / ratio_thr) * (1.0f + 1.0f / 1024.0f);
+#pragma unroll
+    for (int rb = 0; rb < MM_RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+        const float nq = s_nq[w][row];  // +inf (unsafe query): NaN tau, no candidates, full scan
+        // rows past the problem's queries (their A operand repeats the last query) take none:
+        // a fixed radius around |q|^2 = 0 would admit a large share of the references
+        tau[rb][i] = (qw + row < P.nq) ? (R - nq) + fmaf(a1, nq, b2) : -INFINITY;
+      }
+  } else {
   // ---------------- pass 1: an upper bound on the approximate second-best D' per row ----------
   // Each lane keeps the minimum of D' over its own columns; the second-smallest of the 32 lane
   // minima of a row is >= the row's true approximate second-best s' (equal unless the two
@@ -319,7 +351,7 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   float rmax = 0.0f;
   fetch(0);
   stash(0);
-  int buf = 0;
+  buf = 0;
   for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
     __syncthreads();
     const bool more = t0 + MM_RT < nr_all;
@@ -364,7 +396,6 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, m));
-  float tau[MM_RB][16];
 #pragma unroll
   for (int rb = 0; rb < MM_RB; ++rb)
 #pragma unroll
@@ -372,6 +403,8 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
       const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
       tau[rb][i] = s1[rb][i] + 2.0f * mm_bound(s_nq[w][row], rmax);  // inf: every reference
     }
+  __syncthreads();  // every wave is past pass 1's last tile before buffer 0 is refilled
+  }  // pass 1
 
   // ---------------- pass 2: collect the candidates ----------------
   // Candidates are buffered per lane in registers and appended to the LDS lists after the pass
@@ -389,7 +422,6 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
       }
     c_n = 0;
   };
-  __syncthreads();  // every wave is past pass 1's last tile before buffer 0 is refilled
   fetch(0);
   stash(0);
   buf = 0;
@@ -403,6 +435,7 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
       mm_half8 bb[KCH];
       load_b(buf, col, bb);
       float n2 = s_n[buf][1][col];  // -inf: forced candidate
+      if constexpr (RAD) n2 *= 1.0f - a1;
       n2 = (t0 + col < nr_all) ? n2 : INFINITY;  // past the end: never a candidate
 #pragma unroll
       for (int rb = 0; rb < MM_RB; ++rb) {
@@ -502,22 +535,27 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted) {
+                                             float* second_dist, int32_t* accepted, int accept_only) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
+  // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
+  const bool rad = accept_only && dist_thr > 0.0f && dist_thr < 1e30f && ratio_thr > 0.0f && ratio_thr <= 1.0f;
   const char* ex = getenv("PICP_MATCH_EXACT");
   if (ex && atoi(ex) != 0)
     return picp_launch_match(stream, n_problems, max_nq, q_desc, r_desc, probs, dim, dist_thr, ratio_thr,
                              best_idx, best_dist, second_dist, accepted);
   const dim3 g((unsigned)((max_nq + MM_QPB - 1) / MM_QPB), (unsigned)n_problems);
-  if (dim <= 16)
-    hipLaunchKernelGGL(picp_match_mfma_kernel<1>, g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1,
-                       r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                       accepted);
-  else
-    hipLaunchKernelGGL(picp_match_mfma_kernel<2>, g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1,
-                       r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                       accepted);
+#define PICP_LAUNCH_MM(KC, RD)                                                                              \
+  hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1, \
+                     r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted)
+  if (dim <= 16) {
+    if (rad) PICP_LAUNCH_MM(1, 1);
+    else PICP_LAUNCH_MM(1, 0);
+  } else {
+    if (rad) PICP_LAUNCH_MM(2, 1);
+    else PICP_LAUNCH_MM(2, 0);
+  }
+#undef PICP_LAUNCH_MM
   return hipGetLastError();
 }
 

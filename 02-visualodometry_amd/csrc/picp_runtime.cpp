@@ -55,7 +55,13 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted);
+                                             float* second_dist, int32_t* accepted, int accept_only);
+// PICP_MATCH_ACCEPT_ONLY=1 runs picp_match(_batch) in the matcher's accept-only form (what the
+// VO sequence uses) so the tests can check it against the oracle directly
+static int match_accept_only() {
+  const char* e = getenv("PICP_MATCH_ACCEPT_ONLY");
+  return (e && atoi(e) != 0) ? 1 : 0;
+}
 extern "C" int picp_match_prep_kch(int dim);
 extern "C" __global__ void picp_rcp_check_kernel(int e_lo, int e_hi, unsigned long long* bad);
 extern "C" hipError_t picp_launch_essential(hipStream_t stream, const EssArgs* args, const int64_t* offs,
@@ -1266,7 +1272,7 @@ extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1,
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)
     e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
-                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc);
+                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, match_accept_only());
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);

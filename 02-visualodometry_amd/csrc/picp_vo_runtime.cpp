@@ -28,7 +28,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted);
+                                             float* second_dist, int32_t* accepted, int accept_only);
 extern "C" int picp_match_prep_kch(int dim);
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
@@ -76,6 +76,7 @@ struct picp_vo {
   hipGraphExec_t exec = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool use_graph = true;
+  int accept_only = 1;  // the sequence reads only accepted matches (PICP_VO_MATCH_FULL=1: full form)
 };
 
 static void vo_free_segments(picp_vo* h) {
@@ -135,6 +136,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   h->max_obs = mx;
   h->frame_off.assign(frame_off, frame_off + n_frames + 1);
   if (const char* e = getenv("PICP_VO_GRAPH")) h->use_graph = atoi(e) != 0;
+  if (const char* e = getenv("PICP_VO_MATCH_FULL")) h->accept_only = atoi(e) != 0 ? 0 : 1;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
   do {                            \
@@ -331,14 +333,14 @@ static hipError_t vo_enqueue(picp_vo* h) {
     const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, h->pprobs.size() - p0);
     e = picp_launch_match_mfma(h->stream, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1,
                                h->obs_h, h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST,
-                               VO_MATCH_RATIO, h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc);
+                               VO_MATCH_RATIO, h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only);
   }
   if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const VoArgs& V = h->vargs;
   for (int t = 0; t < h->max_steps && e == hipSuccess; ++t) {
     e = picp_launch_match_mfma(h->stream, h->n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
                                V.map_h, V.map_n1, V.map_n2, h->wprobs_d, h->dim, VO_MATCH_DIST,
-                               VO_MATCH_RATIO, h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc);
+                               VO_MATCH_RATIO, h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
     if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
     if (e == hipSuccess)
       e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,

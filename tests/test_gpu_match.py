@@ -7,18 +7,32 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["mfma", "exact"], autouse=True)
+_MODE = {"kernel": "mfma"}
+
+
+@pytest.fixture(params=["mfma", "exact", "accept_only"], autouse=True)
 def matcher_kernel(request, monkeypatch):
-    """Every test runs on both kernels: the MFMA pre-filter (default) and the exact scan
-    (PICP_MATCH_EXACT=1, read at each launch).  Both must give the oracle's bits."""
+    """Every test runs on three forms: the MFMA pre-filter (default) and the exact scan
+    (PICP_MATCH_EXACT=1, read at each launch) must give the oracle's bits; the accept-only
+    radius form the VO sequence runs (PICP_MATCH_ACCEPT_ONLY=1) must give the oracle's accept
+    flags, and its best index and best distance wherever a query is accepted."""
+    monkeypatch.delenv("PICP_MATCH_EXACT", raising=False)
+    monkeypatch.delenv("PICP_MATCH_ACCEPT_ONLY", raising=False)
     if request.param == "exact":
         monkeypatch.setenv("PICP_MATCH_EXACT", "1")
-    else:
-        monkeypatch.delenv("PICP_MATCH_EXACT", raising=False)
+    elif request.param == "accept_only":
+        monkeypatch.setenv("PICP_MATCH_ACCEPT_ONLY", "1")
+    _MODE["kernel"] = request.param
     return request.param
 
 
 def _eq(got, ref):
+    if _MODE["kernel"] == "accept_only":
+        np.testing.assert_array_equal(got["accepted"], ref["accepted"], err_msg="accepted")
+        acc = ref["accepted"].astype(bool)
+        for k in ("best_idx", "best_dist"):
+            np.testing.assert_array_equal(got[k][acc], ref[k][acc], err_msg=k)
+        return
     for k in ("best_idx", "best_dist", "second_dist", "accepted"):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
