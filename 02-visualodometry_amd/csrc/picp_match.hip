@@ -169,6 +169,21 @@ __device__ __forceinline__ float mm_exact_dist(const float* q, const float* __re
   return d;
 }
 
+// The accept-only (radius) form's constants (see the kernel): the per-pair bound's slope a1 and
+// offset b2 (twice mm_bound's headroom) and the radius R = (dist_thr / ratio_thr)(1 + 2^-10).
+#define MM_A1 (3.0f * ((2.0f / 2048.0f + 1.0f / (2048.0f * 2048.0f) + 56.0f / 16777216.0f) + 1.0f / 4194304.0f))
+#define MM_B2 (3.0f / 4194304.0f)
+#define MM_FOLD_MAX 60000.0f  // |x|^2 and |q|^2 bound of the folded form (fp16 range of the halves)
+__device__ __forceinline__ float mm_radius(float dist_thr, float ratio_thr) {
+  return (dist_thr / ratio_thr) * (1.0f + 1.0f / 1024.0f);
+}
+
+// fp16 hi/lo split of x (|x| <= 65504): hi + lo == x to 2^-22 |x| (plus 2^-25 absolute)
+__device__ __forceinline__ void mm_split(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
 // Prep of n descriptors (float[dim] rows): fp16 rows padded to 16*kch, and the two guard norms
 //   n1 = |x|^2, +inf if a component is non-finite or beyond +-60000 (fp16 range): pass 1
 //   n2 = |x|^2, -inf for such a row: pass 2 (an unsafe reference is every query's candidate)
@@ -187,6 +202,16 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
     nr = fmaf(x, x, nr);
   }
   for (int k = 0; k < dp; ++k) h[i * dp + k] = (_Float16)((k < dim && !bad) ? desc[i * dim + k] : 0.0f);
+  if (kch == 1 && dim <= 12) {
+    // the folded radius form's reference-side extension (halves dim .. dim+3, which every query
+    // A operand zeroes outside that form): [-n2s/2 as hi, lo, 1, 1], n2s = |x|^2 (1 - a1)
+    _Float16 hi = (_Float16)0.0f, lo = (_Float16)0.0f;
+    if (!bad && nr <= MM_FOLD_MAX) mm_split(-0.5f * (nr * (1.0f - MM_A1)), hi, lo);
+    h[i * dp + dim] = hi;
+    h[i * dp + dim + 1] = lo;
+    h[i * dp + dim + 2] = (_Float16)1.0f;
+    h[i * dp + dim + 3] = (_Float16)1.0f;
+  }
   n1[i] = bad ? INFINITY : nr;
   n2[i] = bad ? -INFINITY : nr;
 }
@@ -233,6 +258,12 @@ __device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t)
 // best_idx of accepted queries (the VO sequence): pass 1 is skipped and the candidates are the
 // references within a fixed radius of the query (mm_radius below); best_idx, best_dist and
 // second_dist are defined only where accepted[] is 1, accepted[] everywhere.
+// RAD = 2: the same candidates with the radius test FOLDED into the MFMA (dim <= 12): the K
+// slots dim .. dim+3 carry [1, 1, tau/2 hi, tau/2 lo] on the query side and [-n2s/2 hi, lo, 1, 1]
+// on the reference side, so each accumulator element IS S' = q.r - n2s/2 + tau/2 = -S/2 and a
+// reference is a candidate iff S' >= 0; a 32x32 block with no candidate costs one max3 tree and
+// one wave vote instead of 48 VALU.  Tiles holding a reference outside the fold's range
+// (|r|^2 > 60000, unsafe) or past the end take the RAD = 1 compare.
 template <int KCH, int RAD>
 __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
@@ -240,7 +271,8 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     const _Float16* __restrict__ r_h, const float* __restrict__ r_n1, const float* __restrict__ r_n2,
     const MatchProblem* __restrict__ probs, int dim, float dist_thr, float ratio_thr,
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
-    float* __restrict__ second_dist, int32_t* __restrict__ accepted) {
+    float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
+    int xcd_map) {
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
   constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
@@ -262,8 +294,23 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   auto& s_list = lds.list;
   auto& s_nq = lds.nq;
 
-  const MatchProblem P = probs[blockIdx.y];
-  const int64_t q0 = (int64_t)blockIdx.x * MM_QPB;
+  // XCD-aware block order (cdna_hip_programming.md T1): blocks are dealt round-robin over the
+  // 8 XCDs, so block L runs beside blocks L +- 8.  With xcd_map, problem p's query blocks all
+  // get L = p (mod 8): every block of a problem shares one XCD's L2, which then holds the
+  // references of the ~10 problems in flight there instead of a slice of all of them.
+  int pid, qblk;
+  if (xcd_map) {
+    const unsigned L = blockIdx.x, x = L & 7u, sidx = L >> 3;
+    const unsigned pq = sidx / (unsigned)gx;
+    qblk = (int)(sidx - pq * (unsigned)gx);
+    pid = (int)(pq * 8u + x);
+    if (pid >= n_problems) return;
+  } else {
+    pid = blockIdx.y;
+    qblk = blockIdx.x;
+  }
+  const MatchProblem P = probs[pid];
+  const int64_t q0 = (int64_t)qblk * MM_QPB;
   if (q0 >= P.nq) return;  // whole block past this problem
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int64_t qw = q0 + (int64_t)w * MM_QPW;  // this wave's first query
@@ -273,12 +320,18 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   for (int rb = 0; rb < MM_RB; ++rb) {
     const int64_t qi = min(qw + 32 * rb + r, P.nq - 1);
 #pragma unroll
-    for (int c = 0; c < KCH; ++c)
+    for (int c = 0; c < KCH; ++c) {
       qa[rb][c] = *reinterpret_cast<const mm_half8*>(q_h + (P.q_off + qi) * DP + 16 * c + 8 * hf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)  // the prep's fold extension (halves >= dim) is not a component
+        if (16 * c + 8 * hf + e >= dim) qa[rb][c][e] = (_Float16)0.0f;
+    }
   }
   if (lane < MM_QPW) {
     const int64_t qi = qw + lane;
-    s_nq[w][lane] = (qi < P.nq) ? q_n1[P.q_off + qi] : 0.0f;  // +inf: unsafe query
+    float nq = (qi < P.nq) ? q_n1[P.q_off + qi] : 0.0f;  // +inf: unsafe query
+    if (RAD == 2 && !(nq <= MM_FOLD_MAX)) nq = INFINITY;  // outside the fold's range: full scan
+    s_nq[w][lane] = nq;
     s_cnt[w][lane] = 0;
   }
 
@@ -300,6 +353,16 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
       sn[k] = ((idx < MM_RT) ? r_n1 : r_n2)[P.r_off + min(t0 + nt, nr_all - 1)];
     }
   };
+  // RAD = 2: a tile is folded iff it is whole and every reference in it is inside the fold's
+  // range (n1 <= 60000: finite, safe); each thread checks the n1 norms it fetched
+  int my_nofold = 0;
+  auto fold_check = [&](int64_t t0) {
+    int bad = (t0 + MM_RT > nr_all) ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < NPN; ++k)
+      if (tid + k * MM_BLOCK < MM_RT) bad |= (sn[k] <= MM_FOLD_MAX) ? 0 : 1;
+    return bad;
+  };
   auto stash = [&](int b) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) s_t[b][tid + k * MM_BLOCK] = stg[k];
@@ -312,6 +375,7 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   };
 
   float tau[MM_RB][16];
+  mm_half8 qaf[MM_RB];  // RAD = 2: the folded A operands
   float a1 = 0.0f;  // RAD: n2 is scaled by (1 - a1) before the compare (the per-pair bound)
   int buf = 0;
   if constexpr (RAD) {
@@ -324,10 +388,9 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     // only through t = |q|^2 + |r|^2 (Rmax above only bounds |r|^2), E(t) = A t + B, so with
     // twice its headroom (a1 = 2A, 2B) the test D' <= R - |q|^2 + 2E(t) is
     //   fma(-2, q.r, n2 (1 - a1)) <= R - |q|^2 + a1 |q|^2 + 2B.
-    const float v = 1.0f / 2048.0f, u = 1.0f / 16777216.0f, bq = 1.0f / 4194304.0f;
-    a1 = 3.0f * ((2.0f * v + v * v + 56.0f * u) + bq);
-    const float b2 = 3.0f * bq;
-    const float R = (dist_thr / ratio_thr) * (1.0f + 1.0f / 1024.0f);
+    a1 = MM_A1;
+    const float b2 = MM_B2;
+    const float R = mm_radius(dist_thr, ratio_thr);
 #pragma unroll
     for (int rb = 0; rb < MM_RB; ++rb)
 #pragma unroll
@@ -338,6 +401,25 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
         // a fixed radius around |q|^2 = 0 would admit a large share of the references
         tau[rb][i] = (qw + row < P.nq) ? (R - nq) + fmaf(a1, nq, b2) : -INFINITY;
       }
+    if constexpr (RAD == 2) {
+#pragma unroll
+      for (int rb = 0; rb < MM_RB; ++rb) {
+        // A row r of this block: query qw + 32 rb + r (lanes r and 32 + r hold its two halves);
+        // unsafe or out-of-range queries get -2 x 65504 (never a candidate; unsafe ones take
+        // the full scan whatever their candidates)
+        const bool live = qw + 32 * rb + r < P.nq;
+        const float nq = s_nq[w][32 * rb + r];
+        _Float16 th = (_Float16)-65504.0f, tl = (_Float16)-65504.0f;
+        if (live && nq <= MM_FOLD_MAX) mm_split(0.5f * ((R - nq) + fmaf(a1, nq, b2)), th, tl);
+        qaf[rb] = qa[rb][0];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 8 * hf + e;
+          qaf[rb][e] = (k == dim || k == dim + 1) ? (_Float16)1.0f
+                       : (k == dim + 2) ? th : (k == dim + 3) ? tl : qaf[rb][e];
+        }
+      }
+    }
   } else {
   // ---------------- pass 1: an upper bound on the approximate second-best D' per row ----------
   // Each lane keeps the minimum of D' over its own columns; the second-smallest of the 32 lane
@@ -423,12 +505,58 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     c_n = 0;
   };
   fetch(0);
+  if constexpr (RAD == 2) my_nofold = fold_check(0);
   stash(0);
   buf = 0;
   for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
-    __syncthreads();
+    bool fold = false;
+    if constexpr (RAD == 2) fold = __syncthreads_or(my_nofold) == 0;
+    else __syncthreads();
     const bool more = t0 + MM_RT < nr_all;
     if (more) fetch(t0 + MM_RT);
+    if (RAD == 2 && fold) {
+      // folded radius test: element i of the accumulator is S' of (row i, column col)
+#pragma unroll 1
+      for (int sub = 0; sub < MM_RT / 32; ++sub) {
+        const int col = sub * 32 + r;
+        mm_half8 bb[KCH];
+        load_b(buf, col, bb);
+#pragma unroll
+        for (int rb = 0; rb < MM_RB; ++rb) {
+          const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bb[0], (mm_f16v){}, 0, 0, 0);
+          // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
+          // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
+          // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
+          // v_max3 here read the accumulator before the MFMA had written it).
+          int mx = __float_as_int(acc[0]);
+#pragma unroll
+          for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
+          if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
+            unsigned m = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) m = (m << 1) | (__float_as_int(acc[i]) >= 0 ? 1u : 0u);
+            while (m) {
+              const int i = 15 - __builtin_ctz(m);
+              m &= m - 1;
+              if (c_n == MM_LB) flush();
+              const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+#pragma unroll
+              for (int k = 0; k < MM_LB; ++k)
+                if (k == c_n) {
+                  c_row[k] = row;
+                  c_ref[k] = (int)(t0 + col);
+                }
+              ++c_n;
+            }
+          }
+        }
+      }
+      if (more) {
+        my_nofold = fold_check(t0 + MM_RT);  // after the compute: the fetch has landed by now
+        stash(buf ^ 1);
+      }
+      continue;
+    }
 #pragma unroll 1
     for (int sub = 0; sub < MM_RT / 32; ++sub) {
       const int col = sub * 32 + r;
@@ -460,7 +588,10 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
         }
       }
     }
-    if (more) stash(buf ^ 1);
+    if (more) {
+      if constexpr (RAD == 2) my_nofold = fold_check(t0 + MM_RT);
+      stash(buf ^ 1);
+    }
   }
   __syncthreads();
   flush();
@@ -540,16 +671,24 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
   // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
   const bool rad = accept_only && dist_thr > 0.0f && dist_thr < 1e30f && ratio_thr > 0.0f && ratio_thr <= 1.0f;
+  // the folded form needs the extension slots (dim <= 12) and tau/2 inside fp16 range
+  const char* nf = getenv("PICP_MATCH_NO_FOLD");
+  const bool fold = rad && dim <= 12 && (dist_thr / ratio_thr) <= 1000.0f && !(nf && atoi(nf) != 0);
   const char* ex = getenv("PICP_MATCH_EXACT");
   if (ex && atoi(ex) != 0)
     return picp_launch_match(stream, n_problems, max_nq, q_desc, r_desc, probs, dim, dist_thr, ratio_thr,
                              best_idx, best_dist, second_dist, accepted);
-  const dim3 g((unsigned)((max_nq + MM_QPB - 1) / MM_QPB), (unsigned)n_problems);
+  const int gx = (int)((max_nq + MM_QPB - 1) / MM_QPB);
+  const char* xe = getenv("PICP_MATCH_XCD");
+  const int xcd_map = (xe && atoi(xe) == 0) ? 0 : 1;
+  const dim3 g = xcd_map ? dim3((unsigned)(8 * ((n_problems + 7) / 8) * gx)) : dim3((unsigned)gx, (unsigned)n_problems);
 #define PICP_LAUNCH_MM(KC, RD)                                                                              \
   hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1, \
-                     r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted)
+                     r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, \
+                     n_problems, gx, xcd_map)
   if (dim <= 16) {
-    if (rad) PICP_LAUNCH_MM(1, 1);
+    if (fold) PICP_LAUNCH_MM(1, 2);
+    else if (rad) PICP_LAUNCH_MM(1, 1);
     else PICP_LAUNCH_MM(1, 0);
   } else {
     if (rad) PICP_LAUNCH_MM(2, 1);

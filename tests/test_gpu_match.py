@@ -16,8 +16,8 @@ def matcher_kernel(request, monkeypatch):
     (PICP_MATCH_EXACT=1, read at each launch) must give the oracle's bits; the accept-only
     radius form the VO sequence runs (PICP_MATCH_ACCEPT_ONLY=1) must give the oracle's accept
     flags, and its best index and best distance wherever a query is accepted."""
-    monkeypatch.delenv("PICP_MATCH_EXACT", raising=False)
-    monkeypatch.delenv("PICP_MATCH_ACCEPT_ONLY", raising=False)
+    for k in ("PICP_MATCH_EXACT", "PICP_MATCH_ACCEPT_ONLY"):
+        monkeypatch.delenv(k, raising=False)
     if request.param == "exact":
         monkeypatch.setenv("PICP_MATCH_EXACT", "1")
     elif request.param == "accept_only":
@@ -89,6 +89,24 @@ def test_match_empty_and_errors(native):
     assert len(native.match_points(np.zeros((0, 10), np.float32), d)["best_idx"]) == 0
     with pytest.raises(Exception):
         native.match_points(np.ones((4, 33), np.float32), np.ones((4, 33), np.float32))
+
+
+def test_match_large_norm_rows_and_whole_tiles(native, oracle):
+    """Whole 256-row reference tiles and a partial last one; a reference and a query with
+    |x|^2 > 60000 whose components are still inside fp16 range (the bound scales with the
+    norms); a tie and a near match inside a tile; a batch of two problems."""
+    rng = np.random.default_rng(17)
+    d2 = rng.uniform(-1, 1, (3 * 256 + 77, 10)).astype(np.float32)
+    d2[300] = 100.0                      # |r|^2 = 1e5, components inside fp16 range
+    d2[600] = d2[601]                    # a tie inside a whole tile
+    d1 = np.concatenate([d2[[5, 300, 600, 700, 770, 3 * 256 + 70]] + 0.0,
+                         rng.uniform(-1, 1, (200, 10)).astype(np.float32),
+                         np.full((1, 10), 90.0, np.float32)])    # |q|^2 = 81000
+    d1[7] = d2[9] + 0.1                  # near match, |d| = 0.1
+    _eq(native.match_points(d1, d2), oracle.match_points(d1, d2))
+    batch = native.match_points_batch([d1, d1[:50]], [d2, d2[:300]])
+    _eq(batch[0], oracle.match_points(d1, d2))
+    _eq(batch[1], oracle.match_points(d1[:50], d2[:300]))
 
 
 def test_match_adversarial_fallbacks(native, oracle):

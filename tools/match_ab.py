@@ -1,18 +1,34 @@
-import os, sys, time
-sys.path.insert(0, "/root/repo/02-visualodometry_amd")
-import numpy as np
-import picp_amd
+#!/usr/bin/env python3
+"""A/B timing of the matcher forms on one synthetic batch (GPU; profile with rocprofv3
+--kernel-trace to read the per-launch kernel times):
+  python tools/match_ab.py P NQ NR [ENV=v,ENV=v;ENV=v ...]
+Each ';'-separated variant sets its env vars before two timed match_points_batch calls."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "02-visualodometry_amd"))
+import numpy as np  # noqa: E402
+
+import picp_amd  # noqa: E402
+
 rng = np.random.default_rng(0)
 P, nq, nr = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+variants = (sys.argv[4] if len(sys.argv) > 4 else "PICP_MATCH_ACCEPT_ONLY=0;PICP_MATCH_ACCEPT_ONLY=1").split(";")
 d2s = [rng.uniform(-1, 1, (nr, 10)).astype(np.float32) for _ in range(P)]
 d1s = []
 for d2 in d2s:
     d1 = rng.uniform(-1, 1, (nq, 10)).astype(np.float32)
     d1[: nq // 2] = d2[rng.choice(nr, nq // 2, replace=False)]
     d1s.append(d1)
-for mode in ("0", "1", "0", "1"):
-    os.environ["PICP_MATCH_ACCEPT_ONLY"] = mode
-    picp_amd.match_points_batch(d1s, d2s)
-    t = time.perf_counter()
-    out = picp_amd.match_points_batch(d1s, d2s)
-    print(mode, "%.2f ms" % (1e3 * (time.perf_counter() - t)), sum(int(o["accepted"].sum()) for o in out))
+for rep in range(2):
+    for v in variants:
+        for kv in v.split(","):
+            k, val = kv.split("=")
+            os.environ[k] = val
+        picp_amd.match_points_batch(d1s, d2s)
+        t = time.perf_counter()
+        out = picp_amd.match_points_batch(d1s, d2s)
+        print(v, "%.2f ms (incl. copies)" % (1e3 * (time.perf_counter() - t)), sum(int(o["accepted"].sum()) for o in out))
+        for kv in v.split(","):
+            os.environ.pop(kv.split("=")[0], None)
