@@ -516,14 +516,20 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     if (more) fetch(t0 + MM_RT);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
-#pragma unroll 1
+      // the tile's B operands first: one LDS wait per tile instead of one per column block
+      mm_half8 bt[MM_RT / 32];
+#pragma unroll
+      for (int sub = 0; sub < MM_RT / 32; ++sub) {
+        mm_half8 b1[KCH];
+        load_b(buf, sub * 32 + r, b1);
+        bt[sub] = b1[0];
+      }
+#pragma unroll
       for (int sub = 0; sub < MM_RT / 32; ++sub) {
         const int col = sub * 32 + r;
-        mm_half8 bb[KCH];
-        load_b(buf, col, bb);
 #pragma unroll
         for (int rb = 0; rb < MM_RB; ++rb) {
-          const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bb[0], (mm_f16v){}, 0, 0, 0);
+          const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[sub], (mm_f16v){}, 0, 0, 0);
           // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
           // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
           // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
