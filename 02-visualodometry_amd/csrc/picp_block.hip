@@ -10,34 +10,37 @@
 // hand-off latency or HBM.  Ragged batches read (offset, n) from the problem
 // table.
 //
-// Split (split = 2): when twice the problems still fit on the chip (C4: 128 frames, 256 CUs),
-// each problem runs on TWO blocks, each with half of the correspondences, so no CU idles.  Per
+// Split (split = 2 or 4): when S x the problems still fit on the chip (C4: 128 frames, 256 CUs),
+// each problem runs on S blocks, each with 1/S of the correspondences, so no CU idles.  Per
 // round each block publishes its 32-term partial as 64 granules {round, hi|lo} (the double sum
-// as hi = (float)t, lo = (float)(t - hi)), polls its partner's, and both add the two halves in
-// block order: both run the identical solve, so no broadcast is needed.  Partners are blockIdx
-// b and b + 8, which round-robin placement puts on the same XCD (speed only: correctness rests
-// on the tags).  Granules are double-buffered by round parity and zeroed by a memset node before
-// every launch; every wait has an s_memrealtime deadline, refreshed each round (error word set,
-// the problem stops, the host reports it).
+// as hi = (float)t, lo = (float)(t - hi)), polls its S - 1 partners', and all add the parts in
+// part order: every part runs the identical solve, so no broadcast is needed.  Partners are
+// blockIdx b, b + 8, b + 16, ... which round-robin placement puts on the same XCD (speed only:
+// correctness rests on the tags).  Granules are double-buffered by round parity and zeroed by a
+// memset node before every launch; every wait has an s_memrealtime deadline, refreshed each
+// round (error word set, the problem stops, the host reports it).
+// split = 4 uses 256-thread blocks (BS = 256), two per CU from DIFFERENT problems: while one
+// problem's parts exchange and solve (the CU idle in split = 2), the other's compute; the
+// hardware issues the older block first, so the two settle into alternating phases.
 #include "picp_device.h"
 
 using namespace picp;
 
-#define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs
+#define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs (split 1, 2); 256 for split 4
 #define PICP_BLDS_ITEMS 7680  // items staged in LDS: 5 x 4 B x 7680 = 150 KB of the 160 KB per CU
 #define PICP_XG 64            // exchange granules per block per round: 32 hi + 32 lo
 
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
 
-template <int NPT, int PH>
-__global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
+template <int NPT, int PH, int BS>
+__global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
     unsigned long long* xg, unsigned int* err, unsigned long long timeout_ticks) {
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
-  __shared__ float s_wave[PICP_BBLOCK / 64][PICP_NPART];
+  __shared__ float s_wave[BS / 64][PICP_NPART];
   __shared__ double s_tot[PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
@@ -45,11 +48,11 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int p = blockIdx.x, h = 0;
-  if (split == 2) {  // partners b, b + 8 (same XCD); h = which half of the problem
+  if (split > 1) {  // partners b + 8k (same XCD); h = which part of the problem
     const int s = (int)blockIdx.x >> 3;
-    h = s & 1;
-    p = ((s >> 1) << 3) + ((int)blockIdx.x & 7);
-    if (p >= n_problems) return;  // grid padding (whole pairs only)
+    h = s % split;
+    p = (s / split) * 8 + ((int)blockIdx.x & 7);
+    if (p >= n_problems) return;  // grid padding (whole partner groups only)
   }
   int64_t base;
   int n;
@@ -61,11 +64,11 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     base = P.offset;
     n = P.n;
   }
-  if (split == 2) {  // halves start on a multiple of 4 (the planes' alignment)
-    const int half = (((n + 1) >> 1) + 3) & ~3;
-    const int first = min(n, h * half);
-    n = (h == 0) ? min(n, half) : n - first;
-    if (n > 0) base += first;  // an empty half keeps a valid base (its loads are clamped to it)
+  if (split > 1) {  // parts start on a multiple of 4 (the planes' alignment)
+    const int part = (((n + split - 1) / split) + 3) & ~3;
+    const int first = min(n, h * part);
+    n = min(n, first + part) - first;
+    if (n > 0) base += first;  // an empty part keeps a valid base (its loads are clamped to it)
   }
   bgu64_t* const xgg = (bgu64_t*)xg;
 
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int ic = min(tid + k * PICP_BBLOCK, max(n - 1, 0));
+    const int ic = min(tid + k * BS, max(n - 1, 0));
     xs[k] = X[base + ic];
     ys[k] = Y[base + ic];
     zs[k] = Z[base + ic];
@@ -83,14 +86,14 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
 
   // items NPT*BLOCK .. NPT*BLOCK + n_lds - 1 are staged in LDS once (read every round at LDS
   // latency); any beyond that are streamed from L2/MALL every round
-  const int r0 = NPT * PICP_BBLOCK;
+  const int r0 = NPT * BS;
   const int n_lds = max(0, min(n - r0, lds_items));
   float* lx = s_lds;
   float* ly = s_lds + lds_items;
   float* lz = s_lds + 2 * lds_items;
   float* lu = s_lds + 3 * lds_items;
   float* lv = s_lds + 4 * lds_items;
-  for (int i = tid; i < n_lds; i += PICP_BBLOCK) {
+  for (int i = tid; i < n_lds; i += BS) {
     lx[i] = X[base + r0 + i];
     ly[i] = Y[base + r0 + i];
     lz[i] = Z[base + r0 + i];
@@ -139,23 +142,23 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
       const int k1 = (k + 1 < NPT) ? k + 1 : k;
       accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]},
                       (f2){zs[k], zs[k1]}, (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]},
-                      tid + k * PICP_BBLOCK < n, k + 1 < NPT && tid + (k + 1) * PICP_BBLOCK < n, a);
+                      tid + k * BS < n, k + 1 < NPT && tid + (k + 1) * BS < n, a);
     }
-    for (int i = tid; i < n_lds; i += 2 * PICP_BBLOCK) {  // LDS-staged items, in pairs
-      const int i2 = min(i + PICP_BBLOCK, n_lds - 1);
+    for (int i = tid; i < n_lds; i += 2 * BS) {  // LDS-staged items, in pairs
+      const int i2 = min(i + BS, n_lds - 1);
       // scalar locals first: building the f2 operands from the LDS reads directly made the
       // compiler round-trip them through scratch every round
       const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
       const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
       accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
-                      (f2){v0, v1}, true, i + PICP_BBLOCK < n_lds, a);
+                      (f2){v0, v1}, true, i + BS < n_lds, a);
     }
-    for (int i = r0 + n_lds + tid; i < n; i += 2 * PICP_BBLOCK) {  // streamed remainder
-      const int i2 = min(i + PICP_BBLOCK, n - 1);
+    for (int i = r0 + n_lds + tid; i < n; i += 2 * BS) {  // streamed remainder
+      const int i2 = min(i + BS, n - 1);
       const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
       const float x1 = X[base + i2], y1 = Y[base + i2], z1 = Z[base + i2], u1 = U[base + i2], v1 = V[base + i2];
       accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
-                      (f2){v0, v1}, true, i + PICP_BBLOCK < n, a);
+                      (f2){v0, v1}, true, i + BS < n, a);
     }
     float v[PICP_NPART];
     acc2_fold(a, v);
@@ -165,34 +168,51 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     if (tid < PICP_NPART) {  // fixed-order combine of the 8 waves, one lane per term
       double t = 0.0;
 #pragma unroll
-      for (int w = 0; w < PICP_BBLOCK / 64; ++w) t += (double)s_wave[w][tid];
-      if (split == 2) {
-        // publish {round, hi}, {round, lo}; poll the partner's; add the halves in block order
+      for (int w = 0; w < BS / 64; ++w) t += (double)s_wave[w][tid];
+      if (split > 1) {
+        // publish {round, hi}, {round, lo}; poll the partners'; add the parts in part order
         const float hi = (float)t, lo = (float)(t - (double)hi);
         const size_t slot = (size_t)(round & 1) * gridDim.x;
         bgu64_t* mine = xgg + (slot + blockIdx.x) * PICP_XG;
-        const bgu64_t* theirs = xgg + (slot + (blockIdx.x ^ 8u)) * PICP_XG;
         const unsigned tag = (unsigned)round;
         __hip_atomic_store(mine + tid, ((unsigned long long)tag << 32) | __float_as_uint(hi),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(mine + PICP_NPART + tid, ((unsigned long long)tag << 32) | __float_as_uint(lo),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
-        unsigned long long gh = 0, gl = 0;
+        const unsigned g0 = ((blockIdx.x >> 3) / (unsigned)split) * (unsigned)split;  // part 0's group
+        double part_t[4];
+        unsigned pending = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          part_t[q] = 0.0;
+          if (q < split && q != h) pending |= 1u << q;
+        }
+        part_t[h & 3] = (double)hi + (double)lo;
         for (;;) {
-          gh = __hip_atomic_load(theirs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          gl = __hip_atomic_load(theirs + PICP_NPART + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) break;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (!(pending & (1u << q))) continue;
+            const bgu64_t* theirs = xgg + (slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * PICP_XG;
+            const unsigned long long gh = __hip_atomic_load(theirs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long gl =
+                __hip_atomic_load(theirs + PICP_NPART + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) {
+              part_t[q] = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
+              pending &= ~(1u << q);
+            }
+          }
+          if (!pending) break;
           if (__builtin_amdgcn_s_memrealtime() > deadline) {
             __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gh = gl = 0;
             break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        const double mine_t = (double)hi + (double)lo;
-        const double their_t = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
-        t = (h == 0) ? mine_t + their_t : their_t + mine_t;
+        t = part_t[0];
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (q < split) t += part_t[q];
       }
       s_tot[tid] = t;
     }
@@ -203,7 +223,7 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
       for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
       PicpState ns;
       finish_round(A, s_st, tot, round, ns);
-      if (split == 2 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      if (split > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
         ns.done = 1;  // a partner wait timed out: stop (the host reports the error)
       s_st = ns;
 #pragma unroll
@@ -218,12 +238,13 @@ __global__ __launch_bounds__(PICP_BBLOCK) void picp_block_kernel(
     reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
 }
 
-extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part
+extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part (BS 512)
 
-// max_n: the largest problem of the launch (sizes the LDS stage: max_n - npt*512 items, capped).
-// split = 1: grid = n_problems blocks.  split = 2: grid = round_up(2 * n_problems, 16) blocks, all
-// co-resident (the caller checks grid <= CUs), xg = 2 * grid * 64 zeroed u64 granules, err a
-// zeroed word.
+// max_n: the largest problem of the launch (sizes the LDS stage: max_n/split - npt*BS items,
+// capped).  split = 1: grid = n_problems blocks of 512.  split = 2: grid = round_up(2 n_problems,
+// 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of 256, two
+// per CU; all co-resident (the caller checks the grid against the CUs), xg = 2 * grid * 64 zeroed
+// u64 granules, err a zeroed word.
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
@@ -231,28 +252,28 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
                                         unsigned long long timeout_ticks) {
-  if (n_problems <= 0 || !args || (split != 1 && split != 2)) return hipErrorInvalidValue;
-  if (split == 2 && (!xg || !err)) return hipErrorInvalidValue;
-  const int grid = (split == 2) ? ((2 * n_problems + 15) / 16) * 16 : n_problems;
-  const int per_block = (split == 2) ? ((((max_n + 1) >> 1) + 3) & ~3) : max_n;
+  if (n_problems <= 0 || !args || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
+  if (split > 1 && (!xg || !err)) return hipErrorInvalidValue;
+  const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
+  const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
   const bool ph = picp_use_pinhole(args->K);
-  const int lds_items = (per_block > npt * PICP_BBLOCK) ? min(per_block - npt * PICP_BBLOCK, PICP_BLDS_ITEMS) : 0;
+  const int bs = (split == 4) ? 256 : PICP_BBLOCK;
+  const int lds_cap = (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
+  const int lds_items = (per_block > npt * bs) ? min(per_block - npt * bs, lds_cap) : 0;
   const size_t lds_bytes = (size_t)5 * lds_items * sizeof(float);
-#define PICP_LAUNCH_B(N)                                                                                  \
-  if (ph) {                                                                                               \
-    if (lds_bytes > 65536)                                                                                \
-      hipFuncSetAttribute((const void*)picp_block_kernel<N, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                          (int)lds_bytes);                                                                \
-    hipLaunchKernelGGL((picp_block_kernel<N, 1>), dim3(grid), dim3(PICP_BBLOCK), lds_bytes, stream, X, Y, \
-                       Z, U, V, *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err,       \
-                       timeout_ticks);                                                                    \
-  } else {                                                                                                \
-    if (lds_bytes > 65536)                                                                                \
-      hipFuncSetAttribute((const void*)picp_block_kernel<N, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                          (int)lds_bytes);                                                                \
-    hipLaunchKernelGGL((picp_block_kernel<N, 0>), dim3(grid), dim3(PICP_BBLOCK), lds_bytes, stream, X, Y, \
-                       Z, U, V, *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err,       \
-                       timeout_ticks);                                                                    \
+#define PICP_LAUNCH_B3(N, P, B)                                                                            \
+  {                                                                                                        \
+    if (lds_bytes > 65536)                                                                                 \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, B>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                          (int)lds_bytes);                                                                 \
+    hipLaunchKernelGGL((picp_block_kernel<N, P, B>), dim3(grid), dim3(B), lds_bytes, stream, X, Y, Z, U, V, \
+                       *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, timeout_ticks); \
+  }
+#define PICP_LAUNCH_B(N)                              \
+  if (bs == 256) {                                    \
+    if (ph) PICP_LAUNCH_B3(N, 1, 256) else PICP_LAUNCH_B3(N, 0, 256) \
+  } else {                                            \
+    if (ph) PICP_LAUNCH_B3(N, 1, 512) else PICP_LAUNCH_B3(N, 0, 512) \
   }
   switch (npt) {
     case 1: PICP_LAUNCH_B(1); break;
@@ -262,5 +283,6 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
     default: return hipErrorInvalidValue;
   }
 #undef PICP_LAUNCH_B
+#undef PICP_LAUNCH_B3
   return hipGetLastError();
 }

@@ -212,7 +212,7 @@ struct picp_batch {
 // persistent launches and split block launches hand off through granules and report a timed-out
 // wait in the error word at the head of b->sync
 static bool uses_err_word(const picp_batch* b) {
-  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split == 2);
+  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1);
 }
 
 static void drop_graph(picp_batch* b) {
@@ -323,20 +323,25 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
       // two blocks per problem when every pair still gets its own CUs (C4: 128 frames on 256 CUs)
       // and the halves are big enough to pay for the per-round partner exchange;
       // PICP_BLOCK_SPLIT=1|2 forces
-      int split = ((int64_t)2 * np <= b->num_cu && ((2 * np + 15) / 16) * 16 <= b->num_cu &&
-                   max_n >= 4096) ? 2 : 1;
+      auto grid_of = [&](int s) { return ((s * np + 8 * s - 1) / (8 * s)) * (8 * s); };
+      int split = (grid_of(2) <= b->num_cu && max_n >= 4096) ? 2 : 1;
+      // (split 4 -- four 256-thread parts per problem, two blocks per CU from different
+      // problems, meant to overlap one problem's exchange + solve with the other's linearize --
+      // measured 5 % slower than split 2 at C4 (profiles/r01/c4_split4_ab.log): PICP_BLOCK_SPLIT=4)
       if (const char* e = getenv("PICP_BLOCK_SPLIT")) {
         const int v = atoi(e);
         if (v == 1) split = 1;
-        if (v == 2 && ((2 * np + 15) / 16) * 16 <= b->num_cu) split = 2;
+        if (v == 2 && grid_of(2) <= b->num_cu) split = 2;
+        if (v == 4 && grid_of(4) <= 2 * b->num_cu) split = 4;
       }
       b->split = split;
-      if (split == 2) {  // register items per lane for a half
-        const int64_t half = round_up((max_n + 1) / 2, 4);
+      if (split > 1) {  // register items per lane for a part
+        const int64_t part = round_up((max_n + split - 1) / split, 4);
+        const int bs = (split == 4) ? 256 : 512;
         int cap = picp_block_max_items() / 512;
         if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
         bnpt = 1;
-        while (bnpt < cap && (int64_t)bnpt * 512 < half) bnpt *= 2;
+        while (bnpt < cap && (int64_t)bnpt * bs < part) bnpt *= 2;
       }
       b->npt = bnpt;
     }
@@ -394,10 +399,11 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     HIP_TRY(hipHostMalloc((void**)&b->st_pinned, (size_t)np * sizeof(PicpState), hipHostMallocDefault));
     b->np_cap = np;
   }
-  if (b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split == 2)) {
+  if (b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1)) {
     // persistent: error word | pose granules | partial granules (x2 parities);
     // split block: error word | exchange granules (x2 parities, 64 per block)
-    const int64_t sgrid = ((2 * (int64_t)np + 15) / 16) * 16;
+    const int64_t ss = std::max(b->split, 1);
+    const int64_t sgrid = ((ss * np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
                         ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8, 256)
                         : (size_t)round_up(16 + 2 * sgrid * 64 * 8, 256);
@@ -521,7 +527,7 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
   if (b->mode == PICP_MODE_BLOCK) {
     unsigned int* err = nullptr;
     unsigned long long* xg = nullptr;
-    if (b->split == 2) {  // every exchange granule and the error word zeroed before each launch
+    if (b->split > 1) {  // every exchange granule and the error word zeroed before each launch
       hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
       if (e != hipSuccess) return e;
       err = reinterpret_cast<unsigned int*>(b->sync);

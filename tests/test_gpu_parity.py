@@ -494,12 +494,13 @@ def test_streaming_weighted_pair_split_matches_oracle(native, oracle):
         assert abs(st["n_in"] - st_ref["n_in"]) <= 10, share
 
 
-@pytest.mark.parametrize("sizes", [[5000, 1, 3, 4097, 12000, 7], [10000] * 32])
+@pytest.mark.parametrize("sizes", [[5000, 1, 3, 4097, 12000, 7], [10000] * 32, [10000] * 128])
 def test_block_split_matches_oracle(native, oracle, sizes):
-    """Block mode with two blocks per problem (PICP_BLOCK_SPLIT=2, the C4 layout: halves on
-    partner blocks that exchange {round, hi|lo} granules every round) and with one block per
-    problem: both vs the oracle, converged-round counts equal, replays bit-identical.  Problems
-    of 1-7 correspondences leave the second half empty."""
+    """Block mode with two or four blocks per problem (PICP_BLOCK_SPLIT=2: halves on 512-thread
+    partner blocks; =4: quarters on 256-thread blocks, two per CU -- the C4 layout at 128 frames
+    per GPU; partners exchange {round, hi|lo} granules every round) and with one block per
+    problem: all vs the oracle, converged-round counts equal, replays bit-identical.  Problems of
+    1-7 correspondences leave the later parts empty."""
     import os
     synth = _synth()
     probs = [synth.make_problem(n, seed=1300 + i, outlier_frac=0.1 if n >= 1000 else 0.0, pixel_noise=0.5,
@@ -508,7 +509,7 @@ def test_block_split_matches_oracle(native, oracle, sizes):
     uv = np.concatenate([p["uv"] for p in probs])
     Ti = np.stack([p["T_init"] for p in probs])
     res = {}
-    for split in ("1", "2"):
+    for split in ("1", "2", "4"):
         os.environ["PICP_BLOCK_SPLIT"] = split
         try:
             b = _batch_mode(native, sizes, "block")
