@@ -44,6 +44,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
   __shared__ double s_tot[PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
+  __shared__ int s_tmo;  // a partner wait timed out (the error word is for the host)
   __shared__ PicpState s_st;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
 #pragma unroll
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
     s_done = s.done;
+    s_tmo = 0;
     s_st = s;
   }
   __syncthreads();
@@ -205,6 +207,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
           if (!pending) break;
           if (__builtin_amdgcn_s_memrealtime() > deadline) {
             __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_tmo = 1;
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -223,8 +226,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
       PicpState ns;
       finish_round(A, s_st, tot, round, ns);
-      if (split > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-        ns.done = 1;  // a partner wait timed out: stop (the host reports the error)
+      if (s_tmo) ns.done = 1;  // a partner wait timed out: stop (the host reports the error)
       s_st = ns;
 #pragma unroll
       for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];

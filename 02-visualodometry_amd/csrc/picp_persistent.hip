@@ -67,6 +67,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
   __shared__ float s_wave[PICP_PBLOCK / 64][PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
+  __shared__ int s_tmo;  // a wait of this block timed out (the error word is for the host)
   __shared__ PicpState s_st;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
 #pragma unroll
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
     s_done = s.done;
+    s_tmo = 0;
     s_st = s;
     if (leader && s.done) st_out[p] = s;
   }
@@ -207,6 +209,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
         if (!pending) break;
         if (timed_out(deadline)) {
           __hip_atomic_store(errw, 1u, RLX_AGENT);
+          s_tmo = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
           PSTAMP(4);
           finish_round_f(A, s_st, tw, (int)epoch, ns);
           PSTAMP(5);
-          if (__hip_atomic_load(errw, RLX_AGENT) != 0u) ns.done = 1;  // a sweep timed out
+          if (s_tmo) ns.done = 1;  // a sweep timed out
           // ---- publish the new pose (and the done flag): lane l owns word l ----
           float w = 0.0f;
 #pragma unroll
