@@ -41,7 +41,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     unsigned long long* xg, unsigned int* err, unsigned long long timeout_ticks) {
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   __shared__ float s_wave[BS / 64][PICP_NPART];
-  __shared__ double s_tot[PICP_NPART];
+  __shared__ float s_tot[PICP_NPART];  // the totals as finish_round_f words (total_word)
   __shared__ float s_pose[12];
   __shared__ int s_done;
   __shared__ int s_tmo;  // a partner wait timed out (the error word is for the host)
@@ -217,15 +217,15 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
         for (int q = 1; q < 4; ++q)
           if (q < split) t += part_t[q];
       }
-      s_tot[tid] = t;
+      s_tot[tid] = total_word(A, tid, t);  // lane e converts total e
     }
     __syncthreads();
     if (tid == 0) {
-      double tot[PICP_NPART];
+      float tw[PICP_NPART];
 #pragma unroll
-      for (int i = 0; i < PICP_NPART; ++i) tot[i] = s_tot[i];
+      for (int i = 0; i < PICP_NPART; ++i) tw[i] = s_tot[i];
       PicpState ns;
-      finish_round(A, s_st, tot, round, ns);
+      finish_round_f(A, s_st, tw, round, ns);
       if (s_tmo) ns.done = 1;  // a partner wait timed out: stop (the host reports the error)
       s_st = ns;
 #pragma unroll
