@@ -719,8 +719,9 @@ __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState&
 // Two-view linear (DLT) triangulation of one point, cv::triangulatePoints as called from
 // src/cam.cpp:115 then convertPointsFromHomogeneous :118.  P1, P2: 3x4 ROW-major float.
 // A (4x4) in double, right singular vector of the smallest singular value by one-sided
-// (Hestenes) Jacobi with a fixed sweep count; all indices compile-time so A and V stay in
-// registers.
+// (Hestenes) Jacobi, at most 10 sweeps, stopping after the first sweep that rotates nothing
+// (every later sweep would be a no-op, so the result equals the 10-sweep one); all indices
+// compile-time so A and V stay in registers.
 __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 a, float2 b,
                                        float out[3]) {
   double A[4][4], Vm[4][4];
@@ -736,6 +737,7 @@ __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 
 #pragma unroll
     for (int c = 0; c < 4; ++c) Vm[r][c] = (r == c) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 10; ++sweep) {
+    bool rotated = false;  // a sweep that rotates nothing leaves A and V unchanged: stop there
 #pragma unroll
     for (int pq = 0; pq < 6; ++pq) {
       const int p = (pq < 3) ? 0 : ((pq < 5) ? 1 : 2);
@@ -748,6 +750,7 @@ __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 
         gamma += A[k][p] * A[k][qq];
       }
       if (fabs(gamma) > 1e-300 && fabs(gamma) > 1e-17 * sqrt(alpha * beta)) {
+        rotated = true;
         const double zeta = (beta - alpha) / (2.0 * gamma);
         const double t = ((zeta >= 0.0) ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
         const double c = 1.0 / sqrt(1.0 + t * t);
@@ -763,6 +766,7 @@ __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 
         }
       }
     }
+    if (!rotated) break;  // identical result to running all 10 sweeps
   }
   double nrm[4];
 #pragma unroll

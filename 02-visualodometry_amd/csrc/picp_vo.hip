@@ -28,6 +28,11 @@ using namespace picp;
 
 #define VO_BLOCK 256
 #define VO_WAVES (VO_BLOCK / 64)
+// chunks of VO_BLOCK observations whose global loads are all issued before the first ordered
+// compaction step (frames of <= 4096 observations; a larger frame's tail runs the plain loop).
+// One-block-per-segment kernels are latency-bound: loading chunk by chunk between the scan's
+// barriers serialised two dependent global round trips per chunk.
+#define VO_PF 16
 
 // Eigen::Isometry3f::inverse() of a column-major 4x4 (oracle/picp_oracle.c or_iso_inverse order)
 __device__ inline void vo_iso_inverse(const float* T, float* Ti) {
@@ -95,7 +100,42 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
   const int64_t on = a.frame_off[nf], nn = a.frame_off[nf + 1] - on;
   const int64_t moff = G.map_off;
   int64_t cnt = 0;
-  for (int64_t c0 = 0; c0 < nn; c0 += VO_BLOCK) {
+  // every chunk's loads first (accept flag, map index, pixel; then the map point), ...
+  bool fl[VO_PF];
+  float px[VO_PF], py[VO_PF], pz[VO_PF];
+  float2 pu[VO_PF];
+  int jb[VO_PF];
+#pragma unroll
+  for (int c = 0; c < VO_PF; ++c) {
+    const int64_t i = (int64_t)c * VO_BLOCK + threadIdx.x;
+    fl[c] = i < nn && a.wm_acc[on + i] != 0;
+    jb[c] = (i < nn) ? a.wm_bi[on + i] : 0;
+    pu[c] = (i < nn) ? a.uv[on + i] : make_float2(0.0f, 0.0f);
+  }
+#pragma unroll
+  for (int c = 0; c < VO_PF; ++c) {
+    const int64_t j = moff + (fl[c] ? jb[c] : 0);
+    px[c] = fl[c] ? a.map_xyz[3 * j + 0] : 0.0f;
+    py[c] = fl[c] ? a.map_xyz[3 * j + 1] : 0.0f;
+    pz[c] = fl[c] ? a.map_xyz[3 * j + 2] : 0.0f;
+  }
+  // ... then the ordered compaction, chunk by chunk, from registers
+#pragma unroll
+  for (int c = 0; c < VO_PF; ++c) {
+    if ((int64_t)c * VO_BLOCK >= nn) break;  // uniform
+    int tot;
+    const int r = vo_block_rank(fl[c], s_cnt, &tot);
+    if (fl[c]) {
+      const int64_t o = base + cnt + r;
+      a.X[o] = px[c];
+      a.Y[o] = py[c];
+      a.Z[o] = pz[c];
+      a.U[o] = pu[c].x;
+      a.V[o] = pu[c].y;
+    }
+    cnt += tot;
+  }
+  for (int64_t c0 = (int64_t)VO_PF * VO_BLOCK; c0 < nn; c0 += VO_BLOCK) {  // frames > 4096 obs
     const int64_t i = c0 + threadIdx.x;
     const bool flag = i < nn && a.wm_acc[on + i] != 0;
     int tot;
@@ -182,13 +222,34 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
   int2* pairs = a.pairs + (int64_t)s * a.cap_c;
   // pass 1: the selected (curr, next) pairs in pair order (add_new_world_points)
   int64_t cnt = 0;
-  for (int64_t c0 = 0; c0 < nc; c0 += VO_BLOCK) {
+  // every chunk's loads first (accept flag and next index, then the next point's map match), ...
+  bool fl[VO_PF];
+  int jb[VO_PF];
+#pragma unroll
+  for (int c = 0; c < VO_PF; ++c) {
+    const int64_t i = (int64_t)c * VO_BLOCK + threadIdx.x;
+    fl[c] = i < nc && a.pm_acc[oc + i] != 0;
+    jb[c] = (i < nc) ? a.pm_bi[oc + i] : 0;
+  }
+#pragma unroll
+  for (int c = 0; c < VO_PF; ++c)  // next point not among the map correspondences
+    fl[c] = fl[c] && (boot || a.wm_acc[on + (fl[c] ? jb[c] : 0)] == 0);
+  // ... then the ordered compaction from registers
+#pragma unroll
+  for (int c = 0; c < VO_PF; ++c) {
+    if ((int64_t)c * VO_BLOCK >= nc) break;  // uniform
+    int tot;
+    const int r = vo_block_rank(fl[c], s_cnt, &tot);
+    if (fl[c]) pairs[cnt + r] = make_int2(c * VO_BLOCK + (int)threadIdx.x, jb[c]);
+    cnt += tot;
+  }
+  for (int64_t c0 = (int64_t)VO_PF * VO_BLOCK; c0 < nc; c0 += VO_BLOCK) {  // frames > 4096 obs
     const int64_t i = c0 + threadIdx.x;
     bool flag = false;
     int j = 0;
     if (i < nc && a.pm_acc[oc + i]) {
       j = a.pm_bi[oc + i];
-      flag = boot || a.wm_acc[on + j] == 0;  // next point not among the map correspondences
+      flag = boot || a.wm_acc[on + j] == 0;
     }
     int tot;
     const int r = vo_block_rank(flag, s_cnt, &tot);
