@@ -16,7 +16,8 @@
 // Correctness does not depend on placement or timing: only tags are trusted.  Blocks must be
 // co-resident (the host caps the grid at the CU count with ~110 VGPRs / 10 KB LDS per block),
 // every spin is bounded by a per-round s_memrealtime deadline (timeout -> error word, loop exits), and
-// the host zeroes every granule with a memset node before each launch.
+// tags are offset by a per-problem round counter kept on the device (tagbase), so granules left
+// by earlier launches never match and no memset runs between launches.
 #include "picp_device.h"
 
 using namespace picp;
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
-    unsigned long long* gpart, unsigned long long* gpose, unsigned int* err,
+    unsigned long long* gpart, unsigned long long* gpose, unsigned int* err, unsigned int* tagbase,
     unsigned long long timeout_ticks) {
   __shared__ double s_red[PICP_PBLOCK / 64][PICP_NPART + 1];
   __shared__ float s_tot[PICP_NPART];
@@ -85,6 +86,11 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
   gu64_t* prob_part0 = ((gu64_t*)gpart) + (size_t)p * nblk * PICP_NPART;
   gu64_t* prob_pose = ((gu64_t*)gpose) + (size_t)p * PICP_POSE_GRAN;
   gu32_t* errw = ((gu32_t*)err);
+  // Granule tags are tbase + round.  tbase is the problem's count of rounds run by every earlier
+  // launch on these buffers (its leader advances it after the last round), so tags never repeat
+  // and no memset node has to clear the granules before each launch.
+  gu32_t* tbase_p = ((gu32_t*)tagbase) + p;
+  const unsigned tbase = __hip_atomic_load(tbase_p, RLX_AGENT);
 
   // this block's slice, loaded once into registers (coalesced: item = tid + k*BLOCK)
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       float sum = s_wave[0][tid];
 #pragma unroll
       for (int w = 1; w < PICP_PBLOCK / 64; ++w) sum += s_wave[w][tid];
-      __hip_atomic_store(my_part0 + (epoch & 1) * part_stride + tid, granule(epoch, sum), RLX_AGENT);
+      __hip_atomic_store(my_part0 + (epoch & 1) * part_stride + tid, granule(tbase + epoch, sum), RLX_AGENT);
     }
     PSTAMP(1);
 
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
                                                            PICP_AUX_SC1_VOLATILE);
 #pragma unroll
         for (int i = 0; i < MAXG; ++i)
-          if ((want & (1u << i)) && gv[i][1] == epoch && gv[i][3] == epoch) pending &= ~(1u << i);
+          if ((want & (1u << i)) && gv[i][1] == tbase + epoch && gv[i][3] == tbase + epoch) pending &= ~(1u << i);
         if (!pending) break;
         if (timed_out(deadline)) {
           __hip_atomic_store(errw, 1u, RLX_AGENT);
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
 #pragma unroll
           for (int i = 0; i < 3; ++i) w = (lane == 9 + i) ? ns.t[i] : w;
           w = (lane == 12) ? __int_as_float(ns.done) : w;
-          __hip_atomic_store(prob_pose + lane, granule(epoch, w), RLX_AGENT);
+          __hip_atomic_store(prob_pose + lane, granule(tbase + epoch, w), RLX_AGENT);
           if (lane == 0) {
             s_st = ns;
 #pragma unroll
@@ -269,7 +275,12 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
 #pragma unroll
             for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
             s_done = ns.done;
-            if (ns.done) st_out[p] = ns;
+            if (ns.done) {
+              st_out[p] = ns;
+              // every block of the problem read tbase before publishing round 1, and this is
+              // after its last round: the next launch's tags start past this one's
+              __hip_atomic_store(tbase_p, tbase + epoch, RLX_AGENT);
+            }
           }
         }
       }
@@ -283,13 +294,13 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
           bool ok = true;
           if (lane < PICP_POSE_GRAN) {
             gp = __hip_atomic_load(prob_pose + lane, RLX_AGENT);
-            ok = (unsigned)(gp >> 32) == epoch;
+            ok = (unsigned)(gp >> 32) == tbase + epoch;
           }
           if (__all(ok)) break;
           if (timed_out(deadline)) {
             if (lane == 0) __hip_atomic_store(errw, 2u, RLX_AGENT);
-            gp = ((unsigned long long)epoch << 32) | (lane == 12 ? 1u : 0u);  // force done
-            if (lane < 12) gp = ((unsigned long long)epoch << 32) | __float_as_uint(s_pose[lane]);
+            gp = lane == 12 ? 1u : 0u;  // force done
+            if (lane < 12) gp = __float_as_uint(s_pose[lane]);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -319,16 +330,17 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              const float* V, const PicpArgs* args,
                                              const PicpState* st_in, PicpState* st_out,
                                              unsigned long long* gpart, unsigned long long* gpose,
-                                             unsigned int* err, unsigned long long timeout_ticks) {
+                                             unsigned int* err, unsigned int* tagbase,
+                                             unsigned long long timeout_ticks) {
   if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
   const bool ph = picp_use_pinhole(args->K);
 #define PICP_LAUNCH_P(N)                                                                                 \
   if (ph)                                                                                                \
     hipLaunchKernelGGL((picp_persistent_kernel<N, 1>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
-                       U, V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks);                   \
+                       U, V, *args, st_in, st_out, gpart, gpose, err, tagbase, timeout_ticks);                   \
   else                                                                                                   \
     hipLaunchKernelGGL((picp_persistent_kernel<N, 0>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
-                       U, V, *args, st_in, st_out, gpart, gpose, err, timeout_ticks)
+                       U, V, *args, st_in, st_out, gpart, gpose, err, tagbase, timeout_ticks)
   switch (npt) {
     case 1: PICP_LAUNCH_P(1); break;
     case 2: PICP_LAUNCH_P(2); break;

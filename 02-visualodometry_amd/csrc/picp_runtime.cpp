@@ -32,7 +32,8 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              const float* V, const PicpArgs* args,
                                              const PicpState* st_in, PicpState* st_out,
                                              unsigned long long* gpart, unsigned long long* gpose,
-                                             unsigned int* err, unsigned long long timeout_ticks);
+                                             unsigned int* err, unsigned int* tagbase,
+                                             unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
@@ -191,8 +192,9 @@ struct picp_batch {
   int split = 1;               // block mode: blocks per problem (1, or 2 when 2*np fits the chip)
   int mode = PICP_MODE_GRAPH;  // PICP_MODE_GRAPH (launch per round) / PICP_MODE_PERSISTENT
   int npt = 1;                 // persistent: correspondences per lane held in registers
-  unsigned char* sync = nullptr;   // persistent: [err 16 B | pose granules | partial granules]
+  unsigned char* sync = nullptr;   // persistent: [err 16 B | pose granules | partial granules | tag bases]
   size_t sync_bytes = 0, sync_cap = 0;
+  uint64_t tag_rounds = 0;     // persistent: rounds enqueued since the sync area was last zeroed
   int result_idx = 0;          // st_d[] holding the final state of the last solve
   bool last_persistent = false;  // the last solve was a persistent launch (check its error word)
   unsigned long long timeout_ticks = 20000000ull;  // 200 ms of s_memrealtime (100 MHz)
@@ -405,7 +407,8 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     const int64_t ss = std::max(b->split, 1);
     const int64_t sgrid = ((ss * np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
-                        ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8, 256)
+                        ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
+                                               (int64_t)np * 4, 256)
                         : (size_t)round_up(16 + 2 * sgrid * 64 * 8, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
@@ -413,6 +416,9 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
       HIP_TRY(hipMalloc(&b->sync, b->sync_bytes));
       b->sync_cap = b->sync_bytes;
     }
+    // a new layout maps problems onto granules other problems tagged: start every tag from zero
+    HIP_TRY(hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream));
+    b->tag_rounds = 0;
   }
   // block table
   b->blk_h.resize(nblk);
@@ -538,14 +544,15 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
                              b->timeout_ticks);
   }
   if (b->mode == PICP_MODE_PERSISTENT) {
-    // every polled word (error word and all granules) is zeroed before each launch
-    hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
-    if (e != hipSuccess) return e;
+    // no memset per launch: granule tags continue from the per-problem tag bases the previous
+    // launch left (picp_persistent.hip), so nothing a previous launch wrote can match
     unsigned int* err = reinterpret_cast<unsigned int*>(b->sync);
     unsigned long long* gpose = reinterpret_cast<unsigned long long*>(b->sync + 16);
     unsigned long long* gpart = gpose + (size_t)b->np * PICP_POSE_GRAN;
+    unsigned int* tagbase = reinterpret_cast<unsigned int*>(gpart + 2 * (size_t)b->nblk * PICP_NPART);
     return picp_launch_persistent(b->stream, b->nblk, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(),
-                                  &b->args, b->init_d, b->st_d[0], gpart, gpose, err, b->timeout_ticks);
+                                  &b->args, b->init_d, b->st_d[0], gpart, gpose, err, tagbase,
+                                  b->timeout_ticks);
   }
   hipError_t e = graph_prologue(b);
   if (e != hipSuccess) return e;
@@ -571,6 +578,20 @@ static int ensure_graph(picp_batch* b, int R) {
   return PICP_OK;
 }
 
+// Persistent mode: the 32-bit granule tags grow by up to max_rounds per solve.  Zero the sync
+// area (tags and error word) on the stream before they could wrap, i.e. long before 2^32.
+static hipError_t persistent_tag_guard(picp_batch* b, int R, int solves) {
+  if (b->mode != PICP_MODE_PERSISTENT || !b->sync) return hipSuccess;
+  const uint64_t add = (uint64_t)std::max(R, 1) * (uint64_t)solves;
+  if (b->tag_rounds + add > (1ull << 31)) {
+    hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
+    if (e != hipSuccess) return e;
+    b->tag_rounds = 0;
+  }
+  b->tag_rounds += add;
+  return hipSuccess;
+}
+
 static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   HIP_TRY(hipSetDevice(b->device));
   int rc = batch_upload_params(b, prm);
@@ -578,6 +599,7 @@ static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   const int R = prm->max_rounds;
   rc = ensure_graph(b, R);
   if (rc) return rc;
+  HIP_TRY(persistent_tag_guard(b, R, 1));
   HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
   b->last_rounds = R;
   b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
@@ -593,7 +615,14 @@ static int batch_read_results(picp_batch* b) {
     HIP_TRY(hipMemcpyAsync(&err, b->sync, sizeof(err), hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
   memcpy(b->result_h.data(), b->st_pinned, (size_t)b->np * sizeof(PicpState));
-  if (err) return set_err(PICP_ERR_DEVICE, "solve: a cross-block hand-off wait timed out (code %u)", err);
+  if (err) {
+    // the error word is sticky (persistent launches no longer zero it): reset the whole sync
+    // area so the next solve starts clean, then report
+    HIP_TRY(hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    b->tag_rounds = 0;
+    return set_err(PICP_ERR_DEVICE, "solve: a cross-block hand-off wait timed out (code %u)", err);
+  }
   return PICP_OK;
 }
 
@@ -754,6 +783,7 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(persistent_tag_guard(b, R, reps + 1));  // the timed replays and the event-pair solve
   HIP_TRY(hipEventRecord(e0, b->stream));
   for (int r = 0; r < reps; ++r) HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
   HIP_TRY(hipEventRecord(e1, b->stream));
