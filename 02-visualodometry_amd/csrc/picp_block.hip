@@ -38,7 +38,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
-    unsigned long long* xg, unsigned int* err, unsigned long long timeout_ticks) {
+    unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks) {
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   __shared__ float s_wave[BS / 64][PICP_NPART];
   __shared__ float s_tot[PICP_NPART];  // the totals as finish_round_f words (total_word)
@@ -72,6 +72,11 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     if (n > 0) base += first;  // an empty part keeps a valid base (its loads are clamped to it)
   }
   bgu64_t* const xgg = (bgu64_t*)xg;
+  // split: exchange tags are tbase + round, tbase = the rounds this grid slot ran in earlier
+  // launches on these buffers (partners run identical solves, so their bases stay equal); stale
+  // granules never match and no memset has to clear them between launches
+  const unsigned tbase = (split > 1) ? tagbase[blockIdx.x] : 0u;
+  int last_round = 0;
 
   // the problem, loaded once into registers (coalesced: item = tid + k*BLOCK)
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
         const float hi = (float)t, lo = (float)(t - (double)hi);
         const size_t slot = (size_t)(round & 1) * gridDim.x;
         bgu64_t* mine = xgg + (slot + blockIdx.x) * PICP_XG;
-        const unsigned tag = (unsigned)round;
+        const unsigned tag = tbase + (unsigned)round;
         __hip_atomic_store(mine + tid, ((unsigned long long)tag << 32) | __float_as_uint(hi),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(mine + PICP_NPART + tid, ((unsigned long long)tag << 32) | __float_as_uint(lo),
@@ -234,8 +239,11 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
       s_done = ns.done;
     }
+    last_round = round;
     __syncthreads();
   }
+  // every partner read its base before publishing round 1, and has finished its last round
+  if (split > 1 && tid == 0) tagbase[blockIdx.x] = tbase + (unsigned)last_round;
   if (h == 0 && tid < 32)
     reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
 }
@@ -245,17 +253,17 @@ extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // regist
 // max_n: the largest problem of the launch (sizes the LDS stage: max_n/split - npt*BS items,
 // capped).  split = 1: grid = n_problems blocks of 512.  split = 2: grid = round_up(2 n_problems,
 // 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of 256, two
-// per CU; all co-resident (the caller checks the grid against the CUs), xg = 2 * grid * 64 zeroed
-// u64 granules, err a zeroed word.
+// per CU; all co-resident (the caller checks the grid against the CUs), xg = 2 * grid * 64
+// u64 granules, tagbase = grid u32 tag bases (both zeroed once per layout), err the error word.
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
                                         const PicpProblem* probs, const PicpState* st_in,
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
-                                        unsigned long long timeout_ticks) {
+                                        unsigned int* tagbase, unsigned long long timeout_ticks) {
   if (n_problems <= 0 || !args || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
-  if (split > 1 && (!xg || !err)) return hipErrorInvalidValue;
+  if (split > 1 && (!xg || !err || !tagbase)) return hipErrorInvalidValue;
   const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
   const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
   const bool ph = picp_use_pinhole(args->K);
@@ -269,7 +277,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
       hipFuncSetAttribute((const void*)picp_block_kernel<N, P, B>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                           (int)lds_bytes);                                                                 \
     hipLaunchKernelGGL((picp_block_kernel<N, P, B>), dim3(grid), dim3(B), lds_bytes, stream, X, Y, Z, U, V, \
-                       *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, timeout_ticks); \
+                       *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, tagbase, timeout_ticks); \
   }
 #define PICP_LAUNCH_B(N)                              \
   if (bs == 256) {                                    \

@@ -40,7 +40,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         const PicpProblem* probs, const PicpState* st_in,
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
-                                        unsigned long long timeout_ticks);
+                                        unsigned int* tagbase, unsigned long long timeout_ticks);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_persistent_block(void);
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
@@ -409,7 +409,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
                         ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
                                                (int64_t)np * 4, 256)
-                        : (size_t)round_up(16 + 2 * sgrid * 64 * 8, 256);
+                        : (size_t)round_up(16 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
       b->sync = nullptr;
@@ -533,14 +533,16 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
   if (b->mode == PICP_MODE_BLOCK) {
     unsigned int* err = nullptr;
     unsigned long long* xg = nullptr;
-    if (b->split > 1) {  // every exchange granule and the error word zeroed before each launch
-      hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);
-      if (e != hipSuccess) return e;
+    unsigned int* tagbase = nullptr;
+    if (b->split > 1) {  // tags continue from the per-slot tag bases: no memset per launch
+      const int64_t ss = b->split;
+      const int64_t sgrid = ((ss * b->np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
       err = reinterpret_cast<unsigned int*>(b->sync);
       xg = reinterpret_cast<unsigned long long*>(b->sync + 16);
+      tagbase = reinterpret_cast<unsigned int*>(xg + 2 * sgrid * 64);
     }
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
-                             b->probs_d, b->init_d, b->st_d[0], (int)b->max_n, b->split, xg, err,
+                             b->probs_d, b->init_d, b->st_d[0], (int)b->max_n, b->split, xg, err, tagbase,
                              b->timeout_ticks);
   }
   if (b->mode == PICP_MODE_PERSISTENT) {
@@ -578,10 +580,10 @@ static int ensure_graph(picp_batch* b, int R) {
   return PICP_OK;
 }
 
-// Persistent mode: the 32-bit granule tags grow by up to max_rounds per solve.  Zero the sync
-// area (tags and error word) on the stream before they could wrap, i.e. long before 2^32.
+// Persistent and split block modes: the 32-bit granule tags grow by up to max_rounds per solve.
+// Zero the sync area (tags and error word) on the stream before they could wrap (long before 2^32).
 static hipError_t persistent_tag_guard(picp_batch* b, int R, int solves) {
-  if (b->mode != PICP_MODE_PERSISTENT || !b->sync) return hipSuccess;
+  if (!uses_err_word(b) || !b->sync) return hipSuccess;
   const uint64_t add = (uint64_t)std::max(R, 1) * (uint64_t)solves;
   if (b->tag_rounds + add > (1ull << 31)) {
     hipError_t e = hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream);

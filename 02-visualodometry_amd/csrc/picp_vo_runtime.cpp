@@ -36,7 +36,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         const PicpProblem* probs, const PicpState* st_in,
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
-                                        unsigned long long timeout_ticks);
+                                        unsigned int* tagbase, unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
 
@@ -344,7 +344,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
     if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
     if (e == hipSuccess)
       e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,
-                            V.st_in, (PicpState*)V.st_out, (int)h->max_obs, 1, nullptr, nullptr, 0);
+                            V.st_in, (PicpState*)V.st_out, (int)h->max_obs, 1, nullptr, nullptr, nullptr, 0);
     if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &V, t);
   }
   return e;
