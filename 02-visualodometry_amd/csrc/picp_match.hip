@@ -225,6 +225,9 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #ifndef MM_RT
 #define MM_RT 256  // reference rows per LDS tile (128: -3.4 % on C5, 512: -7 %; profiles/r01/match_ab.log)
 #endif
+#ifndef MM_BT
+#define MM_BT 4  // folded pass: column blocks whose B operands are read per LDS wait
+#endif
 // Diagnostic build only (-DPICP_STAMPS): [0] queries through the full-scan fallback, [1] total
 // candidates rescanned, [2] queries, [3] max candidates of a query (tools/match_stats.py).
 #ifdef PICP_STAMPS
@@ -264,8 +267,11 @@ __device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t)
 // reference is a candidate iff S' >= 0; a 32x32 block with no candidate costs one max3 tree and
 // one wave vote instead of 48 VALU.  Tiles holding a reference outside the fold's range
 // (|r|^2 > 60000, unsafe) or past the end take the RAD = 1 compare.
+#ifndef MM_MINB
+#define MM_MINB 1
+#endif
 template <int KCH, int RAD>
-__global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
+__global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
     const _Float16* __restrict__ r_h, const float* __restrict__ r_n1, const float* __restrict__ r_n2,
@@ -346,6 +352,16 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
       const int ch = tid + k * MM_BLOCK;
       const int64_t row = min(t0 + ch / (DP / 8), nr_all - 1);
       stg[k] = *reinterpret_cast<const mm_half8*>(r_h + (P.r_off + row) * DP + (ch % (DP / 8)) * 8);
+      if constexpr (RAD == 2) {
+        // a row past the end folds to S' = -65504 + tau/2 < 0 (never a candidate): components
+        // zero, -n2s/2 hi = -65504, lo = 0, and its [1, 1] slots zero too -- so a partial tile
+        // takes the folded test instead of the compare
+        if (t0 + ch / (DP / 8) >= nr_all) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            stg[k][e] = ((ch % (DP / 8)) * 8 + e == dim) ? (_Float16)-65504.0f : (_Float16)0.0f;
+        }
+      }
     }
 #pragma unroll
     for (int k = 0; k < NPN; ++k) {
@@ -357,7 +373,7 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   // range (n1 <= 60000: finite, safe); each thread checks the n1 norms it fetched
   int my_nofold = 0;
   auto fold_check = [&](int64_t t0) {
-    int bad = (t0 + MM_RT > nr_all) ? 1 : 0;
+    int bad = 0;  // rows past the end are neutralised by fetch (their clamped norms are safe)
 #pragma unroll
     for (int k = 0; k < NPN; ++k)
       if (tid + k * MM_BLOCK < MM_RT) bad |= (sn[k] <= MM_FOLD_MAX) ? 0 : 1;
@@ -378,6 +394,14 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
   mm_half8 qaf[MM_RB];  // RAD = 2: the folded A operands
   float a1 = 0.0f;  // RAD: n2 is scaled by (1 - a1) before the compare (the per-pair bound)
   int buf = 0;
+  // the radius form's threshold of accumulator element i of row block rb
+  auto radius_tau = [&](int rb, int i) {
+    const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+    const float nq = s_nq[w][row];  // +inf (unsafe query): NaN tau, no candidates, full scan
+    // rows past the problem's queries (their A operand repeats the last query) take none:
+    // a fixed radius around |q|^2 = 0 would admit a large share of the references
+    return (qw + row < P.nq) ? (mm_radius(dist_thr, ratio_thr) - nq) + fmaf(MM_A1, nq, MM_B2) : -INFINITY;
+  };
   if constexpr (RAD) {
     // Accept-only (radius) candidates.  With R = (dist_thr / ratio_thr)(1 + 2^-10): a query the
     // reference accepts has its best d* < dist_thr <= R, so every reference at d < R -- the
@@ -391,16 +415,14 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     a1 = MM_A1;
     const float b2 = MM_B2;
     const float R = mm_radius(dist_thr, ratio_thr);
+    // RAD = 2 evaluates tau from LDS inside the (rare) tiles that take the compare -- tiles
+    // with an unsafe reference -- so no 16 registers stay live across the folded loop
+    if constexpr (RAD == 1) {
 #pragma unroll
-    for (int rb = 0; rb < MM_RB; ++rb)
+      for (int rb = 0; rb < MM_RB; ++rb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
-        const float nq = s_nq[w][row];  // +inf (unsafe query): NaN tau, no candidates, full scan
-        // rows past the problem's queries (their A operand repeats the last query) take none:
-        // a fixed radius around |q|^2 = 0 would admit a large share of the references
-        tau[rb][i] = (qw + row < P.nq) ? (R - nq) + fmaf(a1, nq, b2) : -INFINITY;
-      }
+        for (int i = 0; i < 16; ++i) tau[rb][i] = radius_tau(rb, i);
+    }
     if constexpr (RAD == 2) {
 #pragma unroll
       for (int rb = 0; rb < MM_RB; ++rb) {
@@ -516,47 +538,52 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
     if (more) fetch(t0 + MM_RT);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
-      // the tile's B operands first: one LDS wait per tile instead of one per column block
-      mm_half8 bt[MM_RT / 32];
+      // the B operands of MM_BT column blocks first (one LDS wait per group, not per block);
+      // MM_BT = 4 instead of the whole tile keeps 16 registers free for a fifth wave per SIMD
 #pragma unroll
-      for (int sub = 0; sub < MM_RT / 32; ++sub) {
-        mm_half8 b1[KCH];
-        load_b(buf, sub * 32 + r, b1);
-        bt[sub] = b1[0];
-      }
+      for (int sg = 0; sg < MM_RT / 32; sg += MM_BT) {
+        mm_half8 bt[MM_BT];
 #pragma unroll
-      for (int sub = 0; sub < MM_RT / 32; ++sub) {
-        const int col = sub * 32 + r;
+        for (int kb = 0; kb < MM_BT; ++kb) {
+          mm_half8 b1[KCH];
+          load_b(buf, (sg + kb) * 32 + r, b1);
+          bt[kb] = b1[0];
+        }
 #pragma unroll
-        for (int rb = 0; rb < MM_RB; ++rb) {
-          const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[sub], (mm_f16v){}, 0, 0, 0);
-          // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
-          // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
-          // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
-          // v_max3 here read the accumulator before the MFMA had written it).
-          int mx = __float_as_int(acc[0]);
+        for (int kb = 0; kb < MM_BT; ++kb) {
+          const int sub = sg + kb;
+          const int col = sub * 32 + r;
 #pragma unroll
-          for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
-          if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
-            unsigned m = 0;
+          for (int rb = 0; rb < MM_RB; ++rb) {
+            const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[kb], (mm_f16v){}, 0, 0, 0);
+            // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
+            // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
+            // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
+            // v_max3 here read the accumulator before the MFMA had written it).
+            int mx = __float_as_int(acc[0]);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) m = (m << 1) | (__float_as_int(acc[i]) >= 0 ? 1u : 0u);
-            while (m) {
-              const int i = 15 - __builtin_ctz(m);
-              m &= m - 1;
-              if (c_n == MM_LB) flush();
-              const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+            for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
+            if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
+              unsigned m = 0;
 #pragma unroll
-              for (int k = 0; k < MM_LB; ++k)
-                if (k == c_n) {
-                  c_row[k] = row;
-                  c_ref[k] = (int)(t0 + col);
-                }
-              ++c_n;
+              for (int i = 0; i < 16; ++i) m = (m << 1) | (__float_as_int(acc[i]) >= 0 ? 1u : 0u);
+              while (m) {
+                const int i = 15 - __builtin_ctz(m);
+                m &= m - 1;
+                if (c_n == MM_LB) flush();
+                const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
+#pragma unroll
+                for (int k = 0; k < MM_LB; ++k)
+                  if (k == c_n) {
+                    c_row[k] = row;
+                    c_ref[k] = (int)(t0 + col);
+                  }
+                ++c_n;
+              }
             }
           }
         }
-      }
+      }  // column-block group
       if (more) {
         my_nofold = fold_check(t0 + MM_RT);  // after the compute: the fetch has landed by now
         stash(buf ^ 1);
@@ -578,7 +605,8 @@ __global__ __launch_bounds__(MM_BLOCK) void picp_match_mfma_kernel(
         for (int c = 0; c < KCH; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bb[c], acc, 0, 0, 0);
         unsigned m = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) m = mm_shift_in_le(m, fmaf(-2.0f, acc[i], n2), tau[rb][i]);
+        for (int i = 0; i < 16; ++i)
+          m = mm_shift_in_le(m, fmaf(-2.0f, acc[i], n2), RAD == 2 ? radius_tau(rb, i) : tau[rb][i]);
         while (m) {  // rare: the few candidates of this lane's 16 rows (bit 15-i = element i)
           const int i = 15 - __builtin_ctz(m);
           m &= m - 1;
