@@ -33,6 +33,14 @@ using namespace picp;
 // One-block-per-segment kernels are latency-bound: loading chunk by chunk between the scan's
 // barriers serialised two dependent global round trips per chunk.
 #define VO_PF 16
+// The append kernel triangulates with every lane of its block (FP64 Jacobi per new point): a
+// wider block puts four waves on each SIMD instead of one, so the FP64 chains of different
+// points overlap.  Its compaction covers VOA_PF chunks of VOA_BLOCK (4096 observations).
+#ifndef VOA_BLOCK
+#define VOA_BLOCK 512  // 2 waves per SIMD (152 VGPRs); 1024 spills (profiles/r01/vo_append_ab.log)
+#endif
+#define VOA_WAVES (VOA_BLOCK / 64)
+#define VOA_PF (4096 / VOA_BLOCK)
 
 // Eigen::Isometry3f::inverse() of a column-major 4x4 (oracle/picp_oracle.c or_iso_inverse order)
 __device__ inline void vo_iso_inverse(const float* T, float* Ti) {
@@ -70,6 +78,7 @@ __device__ inline void vo_projection(const float* K, const float* Tcw, float* P)
 
 // ordered block compaction: returns this lane's rank among the flagged lanes of the chunk;
 // *total = flagged lanes in the chunk.  Contains two barriers (all lanes must call).
+template <int NW>
 __device__ inline int vo_block_rank(bool flag, int* s_cnt, int* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long m = __ballot(flag);
@@ -78,7 +87,7 @@ __device__ inline int vo_block_rank(bool flag, int* s_cnt, int* total) {
   __syncthreads();
   int pre = 0, tot = 0;
 #pragma unroll
-  for (int k = 0; k < VO_WAVES; ++k) {
+  for (int k = 0; k < NW; ++k) {
     pre += (k < w) ? s_cnt[k] : 0;
     tot += s_cnt[k];
   }
@@ -124,7 +133,7 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
   for (int c = 0; c < VO_PF; ++c) {
     if ((int64_t)c * VO_BLOCK >= nn) break;  // uniform
     int tot;
-    const int r = vo_block_rank(fl[c], s_cnt, &tot);
+    const int r = vo_block_rank<VO_WAVES>(fl[c], s_cnt, &tot);
     if (fl[c]) {
       const int64_t o = base + cnt + r;
       a.X[o] = px[c];
@@ -139,7 +148,7 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
     const int64_t i = c0 + threadIdx.x;
     const bool flag = i < nn && a.wm_acc[on + i] != 0;
     int tot;
-    const int r = vo_block_rank(flag, s_cnt, &tot);
+    const int r = vo_block_rank<VO_WAVES>(flag, s_cnt, &tot);
     if (flag) {
       const int64_t j = moff + a.wm_bi[on + i];
       const int64_t o = base + cnt + r;
@@ -155,7 +164,7 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
   if (threadIdx.x == 0) a.probs[s] = PicpProblem{base, (int32_t)cnt, 0, 1, 0};
 }
 
-__global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int t) {
+__global__ __launch_bounds__(VOA_BLOCK) void vo_append_kernel(const VoArgs a, int t) {
   const int s = blockIdx.x;
   const VoSegment G = a.segs[s];
   const bool boot = t < 0;
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
   __shared__ float sP[24];
   __shared__ float sTn[16];
   __shared__ int64_t s_base;
-  __shared__ int s_cnt[VO_WAVES];
+  __shared__ int s_cnt[VOA_WAVES];
   const int64_t cf = G.f0 + (boot ? 0 : t), nf = cf + 1;
   const int64_t oc = a.frame_off[cf], nc = a.frame_off[cf + 1] - oc;
   const int64_t on = a.frame_off[nf];
@@ -223,27 +232,27 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
   // pass 1: the selected (curr, next) pairs in pair order (add_new_world_points)
   int64_t cnt = 0;
   // every chunk's loads first (accept flag and next index, then the next point's map match), ...
-  bool fl[VO_PF];
-  int jb[VO_PF];
+  bool fl[VOA_PF];
+  int jb[VOA_PF];
 #pragma unroll
-  for (int c = 0; c < VO_PF; ++c) {
-    const int64_t i = (int64_t)c * VO_BLOCK + threadIdx.x;
+  for (int c = 0; c < VOA_PF; ++c) {
+    const int64_t i = (int64_t)c * VOA_BLOCK + threadIdx.x;
     fl[c] = i < nc && a.pm_acc[oc + i] != 0;
     jb[c] = (i < nc) ? a.pm_bi[oc + i] : 0;
   }
 #pragma unroll
-  for (int c = 0; c < VO_PF; ++c)  // next point not among the map correspondences
+  for (int c = 0; c < VOA_PF; ++c)  // next point not among the map correspondences
     fl[c] = fl[c] && (boot || a.wm_acc[on + (fl[c] ? jb[c] : 0)] == 0);
   // ... then the ordered compaction from registers
 #pragma unroll
-  for (int c = 0; c < VO_PF; ++c) {
-    if ((int64_t)c * VO_BLOCK >= nc) break;  // uniform
+  for (int c = 0; c < VOA_PF; ++c) {
+    if ((int64_t)c * VOA_BLOCK >= nc) break;  // uniform
     int tot;
-    const int r = vo_block_rank(fl[c], s_cnt, &tot);
-    if (fl[c]) pairs[cnt + r] = make_int2(c * VO_BLOCK + (int)threadIdx.x, jb[c]);
+    const int r = vo_block_rank<VOA_WAVES>(fl[c], s_cnt, &tot);
+    if (fl[c]) pairs[cnt + r] = make_int2(c * VOA_BLOCK + (int)threadIdx.x, jb[c]);
     cnt += tot;
   }
-  for (int64_t c0 = (int64_t)VO_PF * VO_BLOCK; c0 < nc; c0 += VO_BLOCK) {  // frames > 4096 obs
+  for (int64_t c0 = (int64_t)VOA_PF * VOA_BLOCK; c0 < nc; c0 += VOA_BLOCK) {  // frames > 4096 obs
     const int64_t i = c0 + threadIdx.x;
     bool flag = false;
     int j = 0;
@@ -252,25 +261,41 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_append_kernel(const VoArgs a, int
       flag = boot || a.wm_acc[on + j] == 0;
     }
     int tot;
-    const int r = vo_block_rank(flag, s_cnt, &tot);
+    const int r = vo_block_rank<VOA_WAVES>(flag, s_cnt, &tot);
     if (flag) pairs[cnt + r] = make_int2((int)i, j);
     cnt += tot;
   }
   __syncthreads();
   // pass 2: every lane triangulates (src/cam.cpp:115-139) and appends (xyz, curr descriptor)
-  for (int64_t k = threadIdx.x; k < cnt; k += VO_BLOCK) {
+  for (int64_t k = threadIdx.x; k < cnt; k += VOA_BLOCK) {
     const int2 pr = pairs[k];
     const int64_t slot = mbase + k;
     float o[3];
     triangulate_dlt(sP, sP + 12, a.uv[oc + pr.x], a.uv[on + pr.y], o);
+    // the descriptor row and the matcher's prepped row of it (fp16 + guard norms): every load
+    // first, then the stores -- the compiler cannot rule out that a store aliases a later load,
+    // so an interleaved element copy paid one global round trip per element
+    const int64_t src = oc + pr.x;
+    float dv[32];  // dim <= 32 (picp_vo_create)
+#pragma unroll
+    for (int d = 0; d < 32; ++d) dv[d] = (d < dim) ? a.desc[src * dim + d] : 0.0f;
+    uint4 hv[4];  // dp = 16 or 32 halves: dp / 8 chunks of 16 B (rows 32-B aligned)
+    const uint4* hs = reinterpret_cast<const uint4*>(a.obs_h + src * a.dp);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) hv[c] = (c < a.dp / 8) ? hs[c] : make_uint4(0u, 0u, 0u, 0u);
+    const float n1 = a.obs_n1[src], n2 = a.obs_n2[src];
     a.map_xyz[3 * slot + 0] = o[0];
     a.map_xyz[3 * slot + 1] = o[1];
     a.map_xyz[3 * slot + 2] = o[2];
-    for (int d = 0; d < dim; ++d) a.map_desc[slot * dim + d] = a.desc[(oc + pr.x) * dim + d];
-    // the matcher's prepped row of the same descriptor (fp16 + guard norms)
-    for (int d = 0; d < a.dp; ++d) a.map_h[slot * a.dp + d] = a.obs_h[(oc + pr.x) * a.dp + d];
-    a.map_n1[slot] = a.obs_n1[oc + pr.x];
-    a.map_n2[slot] = a.obs_n2[oc + pr.x];
+#pragma unroll
+    for (int d = 0; d < 32; ++d)
+      if (d < dim) a.map_desc[slot * dim + d] = dv[d];
+    uint4* hd = reinterpret_cast<uint4*>(a.map_h + slot * a.dp);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < a.dp / 8) hd[c] = hv[c];
+    a.map_n1[slot] = n1;
+    a.map_n2[slot] = n2;
   }
   if (threadIdx.x == 0) {
     const int64_t mn = s_base + cnt;
@@ -312,6 +337,6 @@ extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a,
 
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t) {
   if (!a || a->n_seg <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(vo_append_kernel, dim3(a->n_seg), dim3(VO_BLOCK), 0, stream, *a, t);
+  hipLaunchKernelGGL(vo_append_kernel, dim3(a->n_seg), dim3(VOA_BLOCK), 0, stream, *a, t);
   return hipGetLastError();
 }
