@@ -32,6 +32,26 @@ using namespace picp;
 
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
 
+// Diagnostic build only (-DPICP_STAMPS): s_memrealtime per phase of rounds 11 and 12 seen by
+// thread 0 of blocks < 256 (tools/bstamps.py).
+#ifdef PICP_STAMPS
+__device__ unsigned long long picp_bstamps[2][256][8];
+#define BSTAMP(k)                                                                               \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && (round == 11 || round == 12) && blockIdx.x < 256)                    \
+      picp_bstamps[round - 11][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                \
+  } while (0)
+extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words) {
+  const size_t cap = sizeof(picp_bstamps) / sizeof(unsigned long long);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_bstamps), (n_words < cap ? n_words : cap) * 8, 0,
+                             hipMemcpyDeviceToHost);
+}
+#else
+#define BSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 template <int NPT, int PH, int BS>
 __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
@@ -137,6 +157,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
   const bool keep = A.keep_outliers != 0;
 
   for (int round = 1; !s_done; ++round) {
+    BSTAMP(0);
     Pose T;
     T.r00 = s_pose[0]; T.r10 = s_pose[1]; T.r20 = s_pose[2];
     T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
@@ -168,10 +189,13 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
                       (f2){v0, v1}, true, i + BS < n, a);
     }
     float v[PICP_NPART];
+    BSTAMP(1);
     acc2_fold(a, v);
     const float wsum = wave_reduce32(v, lane);
     if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
+    BSTAMP(2);
     __syncthreads();
+    BSTAMP(3);
     if (tid < PICP_NPART) {  // fixed-order combine of the 8 waves, one lane per term
       double t = 0.0;
 #pragma unroll
@@ -224,7 +248,10 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       }
       s_tot[tid] = total_word(A, tid, t);  // lane e converts total e
     }
-    __syncthreads();
+    // the totals (and s_tmo) were written by lanes < 32 of wave 0, which also runs the solve:
+    // a wave barrier orders them, the other waves wait at the block barrier after the solve
+    __builtin_amdgcn_wave_barrier();
+    BSTAMP(4);
     if (tid == 0) {
       float tw[PICP_NPART];
 #pragma unroll
@@ -239,8 +266,10 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
       s_done = ns.done;
     }
+    BSTAMP(5);
     last_round = round;
     __syncthreads();
+    BSTAMP(6);
   }
   // every partner read its base before publishing round 1, and has finished its last round
   if (split > 1 && tid == 0) tagbase[blockIdx.x] = tbase + (unsigned)last_round;
