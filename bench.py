@@ -143,9 +143,12 @@ def main():
     corr_per_launch = int(info["total_corr"]) * (1 if info["mode"] == "graph" else R)
     achieved = BYTES_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
 
-    traffic, tsrc = (pmc_traffic("c2_persistent")
-                     if (args.workload == "c2" and n == 100000 and len(sizes) == 1 and R == 50
-                         and info["mode"] == "persistent") else (None, None))
+    # HBM traffic per launch from the committed PMC passes of the same default command
+    # (tools/gpu_pmc.sh): C2 / C3 persistent kernel, C4 block kernel
+    pmc_name = {("c2", "persistent"): "c2_persistent", ("c3", "persistent"): "c3_persistent",
+                ("c4", "block"): "c4_block"}.get((args.workload, info["mode"]))
+    default_cfg = (n == wl["n"] and len(sizes) == wl["problems"] and R == 50)
+    traffic, tsrc = pmc_traffic(pmc_name) if (pmc_name and default_cfg) else (None, None)
     rounds_total = world * len(sizes) * R * args.steps
     value = rounds_total / elapsed
     out = {
@@ -202,6 +205,21 @@ def main():
             "conv_eps": 1e-5, "rounds_run": rounds_run, "ms_per_solve": round(per_solve_ms, 4),
             "iterations_per_s": round(len(sizes) * rounds_run / (per_solve_ms * 1e-3), 1),
             "pose_err_vs_gt_se3": max(synth.se3_log_norm(b.poses()[i], T_gt[i]) for i in range(len(sizes))),
+        }
+    if args.workload == "c3" and not args.skip_extras:
+        # also with keep_outliers = true (outliers weighted by the robust
+        # lambda = sqrt(threshold / chi), src/picp_solver.cpp:80-88), measured after the timed region
+        kparams = dict(params, keep_outliers=1)
+        b.set_poses(T_init)
+        b.solve(**kparams)
+        kerr = max(synth.se3_log_norm(b.poses()[i], T_gt[i]) for i in range(len(sizes)))
+        kms, _ = b.time(args.steps, **kparams)
+        out["keep_outliers_true"] = {
+            "rounds": R, "ms_per_solve": round(kms / args.steps, 4),
+            "iterations_per_s": round(len(sizes) * R / (kms / args.steps * 1e-3), 1),
+            "pose_err_vs_gt_se3": kerr,
+            "note": "outliers are weighted by the robust lambda, not rejected: the pose is biased by them "
+                    "by design (the reference's keep_outliers mode); parity with the oracle is tested",
         }
     if args.workload == "c2" and args.stream_n > 0 and world == 1:
         out["roofline_streaming"] = streaming_roofline(args.stream_n, R, thr, local if world > 1 else 0)
