@@ -373,6 +373,7 @@ def bench_vo(args, wl, world, rank, local, dist, torch):
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
+        out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:
@@ -402,6 +403,38 @@ def cpu_baseline_vo(seq, L, budget_s):
     return {"value": round(frames / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": "%d frames in %d-step segments of the same sequence (oracle VO loop, faithful "
                       "float32, gcc -O3, 1 thread) in %.1f s" % (frames, L, el)}
+
+
+def cpu_baseline_vo_mt(seq, L, budget_s):
+    """SURVEY.md §8d all-cores variant of the C5 baseline: the oracle VO loop over independent
+    segments in parallel, one segment per host thread (OMP_NUM_THREADS threads, 16 = the GPU box's
+    CPU share).  ctypes releases the GIL around or_vo_segment, whose VO path keeps no static
+    state, so the threads run concurrently.  Timing only, never a parity oracle."""
+    import concurrent.futures as cf
+    import numpy as np
+    import oracle as O
+    nt = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 64))
+    D = seq.frames(0, min(seq.n_frames, nt * L + 1))
+    nseg = max(1, (len(D["frame_off"]) - 2) // L)
+    t0 = time.perf_counter()
+
+    def worker(i):
+        f0 = (i % nseg) * L
+        st = min(L, len(D["frame_off"]) - 2 - f0)
+        T1 = (np.linalg.inv(D["T_cw"][f0].astype(np.float64)) @ D["T_cw"][f0 + 1]).astype(np.float32)
+        done = 0
+        while time.perf_counter() - t0 < budget_s:
+            O.vo_segment(seq.K, 480, 640, D["frame_off"], D["uv"], D["desc"], f0, st,
+                         np.eye(4, dtype=np.float32), T1, mode=O.MODE_FAITHFUL)
+            done += st
+        return done
+
+    with cf.ThreadPoolExecutor(max_workers=nt) as ex:
+        frames = sum(ex.map(worker, range(nt)))
+    el = time.perf_counter() - t0
+    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": nt, "kind": "port",
+            "sample": "%d frames: %d threads, each re-running one %d-step segment of the same sequence "
+                      "(oracle VO loop, faithful float32, gcc -O3) for %.1f s on %s" % (frames, nt, L, el, _cpu_model())}
 
 
 def _cpu_model():
