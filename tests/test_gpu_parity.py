@@ -413,9 +413,45 @@ def test_uniform_multi_frame_batch_modes(native, oracle, mode, P, n):
                                          max_rounds=50, conv_eps=1e-5)
         assert synth.se3_log_norm(poses[i], T_ref) < POSE_TOL
         assert stats[i]["converged"] == int(st_ref["converged"])
-    # repeated replays of the same graph give identical results (granules re-zeroed per launch)
+    # repeated replays of the same graph give identical results (persistent / split block: the
+    # granule tags continue from the tag bases the previous launch left, nothing is re-zeroed)
     b.solve(threshold=THR, max_rounds=50, conv_eps=1e-5)
     np.testing.assert_array_equal(b.poses(), poses)
+
+
+@pytest.mark.parametrize("mode,P,n,split", [("persistent", 1, 100000, None), ("persistent", 4, 5000, None),
+                                            ("block", 8, 8192, "2"), ("block", 8, 8192, "4")])
+def test_tag_bases_across_launches(native, mode, P, n, split):
+    """Persistent and split-block launches run without a memset between them: every solve's
+    granule tags start past the previous launch's.  Interleave solves of 0, 1, 7 and 50 rounds
+    and convergence-terminated ones (rounds differ per problem) on ONE batch, each compared
+    bit for bit with the same solve on a fresh batch."""
+    import os
+    synth = _synth()
+    bt = synth.make_batch(P, n, base_seed=900, pixel_noise=0.5, outlier_frac=0.1)
+    old = os.environ.get("PICP_BLOCK_SPLIT")
+    if split:
+        os.environ["PICP_BLOCK_SPLIT"] = split
+    try:
+        def fresh():
+            b = _batch_mode(native, bt["sizes"], mode)
+            b.set_data(bt["xyz"], bt["uv"])
+            b.set_poses(bt["T_init"])
+            return b
+        b = fresh()
+        assert b.info()["mode"] == mode
+        plan = [(50, -1.0), (0, -1.0), (7, -1.0), (1, -1.0), (50, 1e-5), (50, -1.0), (7, 1e-3), (50, 1e-5)]
+        for R, eps in plan:
+            b.solve(threshold=THR, max_rounds=R, conv_eps=eps)
+            f = fresh()
+            f.solve(threshold=THR, max_rounds=R, conv_eps=eps)
+            np.testing.assert_array_equal(b.poses(), f.poses(), err_msg="R=%d eps=%g" % (R, eps))
+            assert [s["rounds"] for s in b.stats()] == [s["rounds"] for s in f.stats()]
+    finally:
+        if old is None:
+            os.environ.pop("PICP_BLOCK_SPLIT", None)
+        else:
+            os.environ["PICP_BLOCK_SPLIT"] = old
 
 
 def test_fast_reciprocal_is_correctly_rounded(native):
