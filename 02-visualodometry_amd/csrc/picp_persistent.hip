@@ -28,9 +28,6 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #define PICP_MAX_PBLK 256   // max blocks per problem in this mode (sweep registers)
 #define PICP_PBLOCK 512     // threads per block: 8 waves, 2 per SIMD (<= 256 VGPRs)
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
-#ifndef PICP_POLL_PIPE
-#define PICP_POLL_PIPE 1    // non-leader blocks keep two pose polls in flight
-#endif
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
 // never hoisted out of a spin loop)
 #define PICP_AUX_SC1_VOLATILE ((int)(16u | 0x80000000u))
@@ -293,31 +290,6 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       // ---- 3. wait for the leader's pose of this round (one wave, 16 lanes) ----
       if (wave == 0) {
         unsigned long long gp = 0;
-#if PICP_POLL_PIPE
-        // two polls in flight: the next load is issued before the older one's tags are checked,
-        // so a pose that lands between polls is seen about half a round trip sooner.  Every lane
-        // loads (lanes >= 16 repeat the first 16 granules: one 128-B line, no exec branch).
-        // Unrolled by two with fixed registers (a rotation would make the compiler wait for
-        // every load in flight before the move).
-        const gu64_t* src = prob_pose + (lane & (PICP_POSE_GRAN - 1));
-        const unsigned want = tbase + epoch;
-        bool tmo = false;
-        unsigned long long g0 = __hip_atomic_load(src, RLX_AGENT);
-        unsigned long long g1 = __hip_atomic_load(src, RLX_AGENT);
-        for (;;) {
-          if (__all((unsigned)(g0 >> 32) == want)) { gp = g0; break; }
-          if (timed_out(deadline)) { tmo = true; break; }
-          g0 = __hip_atomic_load(src, RLX_AGENT);
-          if (__all((unsigned)(g1 >> 32) == want)) { gp = g1; break; }
-          if (timed_out(deadline)) { tmo = true; break; }
-          g1 = __hip_atomic_load(src, RLX_AGENT);
-        }
-        if (tmo) {
-          if (lane == 0) __hip_atomic_store(errw, 2u, RLX_AGENT);
-          gp = lane == 12 ? 1u : 0u;  // force done
-          if (lane < 12) gp = __float_as_uint(s_pose[lane]);
-        }
-#else
         for (;;) {
           bool ok = true;
           if (lane < PICP_POSE_GRAN) {
@@ -333,7 +305,6 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
           }
           __builtin_amdgcn_s_sleep(1);
         }
-#endif
         if (lane < 12) s_pose[lane] = __uint_as_float((unsigned)gp);
         if (lane == 12) s_done = (int)(unsigned)gp;
       }
