@@ -144,11 +144,9 @@ typedef float mm_f16v __attribute__((ext_vector_type(16)));
 #define MM_WAVES 4
 #endif
 #define MM_BLOCK (64 * MM_WAVES)
-#ifndef MM_RB
-#define MM_RB 1                   // 32-query MFMA row blocks per wave (share every B operand)
-#endif
-#define MM_QPW (32 * MM_RB)       // queries per wave
-#define MM_QPB (MM_WAVES * MM_QPW)
+// RB (kernel template argument): 32-query MFMA row blocks per wave, sharing every B operand.
+// The launcher takes RB = 2 when that still fills a generation of blocks (C5: +3.4 %,
+// 1024 x 2000 x 2000: -9 % time) and RB = 1 for small grids (64 x 2000 x 8000: RB = 2 +9 %).
 #define MM_CAP 16                 // candidate slots per query
 #define MM_SAFE 60000.0f
 
@@ -270,7 +268,7 @@ __device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t)
 #ifndef MM_MINB
 #define MM_MINB 1
 #endif
-template <int KCH, int RAD>
+template <int KCH, int RAD, int RB>
 __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
@@ -279,6 +277,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
     float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
     int xcd_map) {
+  constexpr int QPW = 32 * RB;                      // queries per wave
+  constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
   constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
@@ -289,9 +289,9 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   struct Lds {
     mm_half8 t[2][CH];                   // tile rows, 16-B chunks: row*(DP/8) + c*2 + h
     float n[2][2][MM_RT];                // [buf][n1|n2][ref]
-    int cnt[MM_WAVES][MM_QPW];
-    int list[MM_WAVES][MM_QPW][MM_CAP];
-    float nq[MM_WAVES][MM_QPW];
+    int cnt[MM_WAVES][QPW];
+    int list[MM_WAVES][QPW][MM_CAP];
+    float nq[MM_WAVES][QPW];
   };
   __shared__ Lds lds;
   auto& s_t = lds.t;
@@ -316,14 +316,14 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     qblk = blockIdx.x;
   }
   const MatchProblem P = probs[pid];
-  const int64_t q0 = (int64_t)qblk * MM_QPB;
+  const int64_t q0 = (int64_t)qblk * QPB;
   if (q0 >= P.nq) return;  // whole block past this problem
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
-  const int64_t qw = q0 + (int64_t)w * MM_QPW;  // this wave's first query
+  const int64_t qw = q0 + (int64_t)w * QPW;  // this wave's first query
 
-  mm_half8 qa[MM_RB][KCH];  // A operands: query qw + 32 rb + r, halves [16c + 8 hf, +8)
+  mm_half8 qa[RB][KCH];  // A operands: query qw + 32 rb + r, halves [16c + 8 hf, +8)
 #pragma unroll
-  for (int rb = 0; rb < MM_RB; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     const int64_t qi = min(qw + 32 * rb + r, P.nq - 1);
 #pragma unroll
     for (int c = 0; c < KCH; ++c) {
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         if (16 * c + 8 * hf + e >= dim) qa[rb][c][e] = (_Float16)0.0f;
     }
   }
-  if (lane < MM_QPW) {
+  if (lane < QPW) {
     const int64_t qi = qw + lane;
     float nq = (qi < P.nq) ? q_n1[P.q_off + qi] : 0.0f;  // +inf: unsafe query
     if (RAD == 2 && !(nq <= MM_FOLD_MAX)) nq = INFINITY;  // outside the fold's range: full scan
@@ -390,8 +390,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     for (int c = 0; c < KCH; ++c) bb[c] = s_t[b][col * (DP / 8) + 2 * c + hf];
   };
 
-  float tau[MM_RB][16];
-  mm_half8 qaf[MM_RB];  // RAD = 2: the folded A operands
+  float tau[RB][16];
+  mm_half8 qaf[RB];  // RAD = 2: the folded A operands
   float a1 = 0.0f;  // RAD: n2 is scaled by (1 - a1) before the compare (the per-pair bound)
   int buf = 0;
   // the radius form's threshold of accumulator element i of row block rb
@@ -419,13 +419,13 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     // with an unsafe reference -- so no 16 registers stay live across the folded loop
     if constexpr (RAD == 1) {
 #pragma unroll
-      for (int rb = 0; rb < MM_RB; ++rb)
+      for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tau[rb][i] = radius_tau(rb, i);
     }
     if constexpr (RAD == 2) {
 #pragma unroll
-      for (int rb = 0; rb < MM_RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         // A row r of this block: query qw + 32 rb + r (lanes r and 32 + r hold its two halves);
         // unsafe or out-of-range queries get -2 x 65504 (never a candidate; unsafe ones take
         // the full scan whatever their candidates)
@@ -447,9 +447,9 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   // Each lane keeps the minimum of D' over its own columns; the second-smallest of the 32 lane
   // minima of a row is >= the row's true approximate second-best s' (equal unless the two
   // smallest share a lane), so tau below can only be looser -- more candidates, same result.
-  float b1[MM_RB][16], s1[MM_RB][16];
+  float b1[RB][16], s1[RB][16];
 #pragma unroll
-  for (int rb = 0; rb < MM_RB; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) b1[rb][i] = s1[rb][i] = INFINITY;
   float rmax = 0.0f;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       rmax = (na < INFINITY && na > rmax) ? na : rmax;
       rmax = (nb < INFINITY && nb > rmax) ? nb : rmax;
 #pragma unroll
-      for (int rb = 0; rb < MM_RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         mm_f16v acc_a = {}, acc_b = {};
 #pragma unroll
         for (int c = 0; c < KCH; ++c) {
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
   for (int m = 1; m < 32; m <<= 1) {
 #pragma unroll
-    for (int rb = 0; rb < MM_RB; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float pb = __shfl_xor(b1[rb][i], m), ps = __shfl_xor(s1[rb][i], m);
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, m));
 #pragma unroll
-  for (int rb = 0; rb < MM_RB; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
           const int sub = sg + kb;
           const int col = sub * 32 + r;
 #pragma unroll
-          for (int rb = 0; rb < MM_RB; ++rb) {
+          for (int rb = 0; rb < RB; ++rb) {
             const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[kb], (mm_f16v){}, 0, 0, 0);
             // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
             // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
@@ -599,7 +599,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       if constexpr (RAD) n2 *= 1.0f - a1;
       n2 = (t0 + col < nr_all) ? n2 : INFINITY;  // past the end: never a candidate
 #pragma unroll
-      for (int rb = 0; rb < MM_RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         mm_f16v acc = {};
 #pragma unroll
         for (int c = 0; c < KCH; ++c) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qa[rb][c], bb[c], acc, 0, 0, 0);
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 
   // ---------------- exact update over the candidates, in index order ----------------
   const int64_t qi = qw + lane;
-  if (lane < MM_QPW && qi < P.nq) {
+  if (lane < QPW && qi < P.nq) {
     float q[DMAX];
 #pragma unroll
     for (int k = 0; k < DMAX; ++k) q[k] = (k < dim) ? q_desc[(P.q_off + qi) * dim + k] : 0.0f;
@@ -712,22 +712,43 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   if (ex && atoi(ex) != 0)
     return picp_launch_match(stream, n_problems, max_nq, q_desc, r_desc, probs, dim, dist_thr, ratio_thr,
                              best_idx, best_dist, second_dist, accepted);
-  const int gx = (int)((max_nq + MM_QPB - 1) / MM_QPB);
+  // RB = 2 (64 queries per wave) halves the tile fetches and LDS B reads per query but also the
+  // block count: take it when the grid still holds a full generation (4 blocks per CU at the
+  // folded form's 109 VGPRs).  PICP_MATCH_RB=1|2 forces.
+  static int num_cu = 0;
+  if (!num_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cu <= 0)
+      num_cu = 256;
+  }
+  const int64_t blocks_rb2 = (int64_t)n_problems * ((max_nq + 2 * 32 * MM_WAVES - 1) / (2 * 32 * MM_WAVES));
+  // (measured for the folded accept-only form only; the others need 130-224 VGPRs at RB = 2)
+  int rb = (fold && blocks_rb2 >= 4 * (int64_t)num_cu) ? 2 : 1;
+  if (const char* e = getenv("PICP_MATCH_RB")) rb = (atoi(e) == 2) ? 2 : 1;
+  const int qpb = MM_WAVES * 32 * rb;
+  const int gx = (int)((max_nq + qpb - 1) / qpb);
   const char* xe = getenv("PICP_MATCH_XCD");
   const int xcd_map = (xe && atoi(xe) == 0) ? 0 : 1;
   const dim3 g = xcd_map ? dim3((unsigned)(8 * ((n_problems + 7) / 8) * gx)) : dim3((unsigned)gx, (unsigned)n_problems);
-#define PICP_LAUNCH_MM(KC, RD)                                                                              \
-  hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h, q_n1, \
-                     r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, \
-                     n_problems, gx, xcd_map)
-  if (dim <= 16) {
-    if (fold) PICP_LAUNCH_MM(1, 2);
-    else if (rad) PICP_LAUNCH_MM(1, 1);
-    else PICP_LAUNCH_MM(1, 0);
-  } else {
-    if (rad) PICP_LAUNCH_MM(2, 1);
-    else PICP_LAUNCH_MM(2, 0);
+#define PICP_LAUNCH_MM3(KC, RD, R)                                                                          \
+  hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD, R>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h,  \
+                     q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, \
+                     accepted, n_problems, gx, xcd_map)
+#define PICP_LAUNCH_MM(KC, RD)                   \
+  {                                              \
+    if (rb == 2) PICP_LAUNCH_MM3(KC, RD, 2);     \
+    else PICP_LAUNCH_MM3(KC, RD, 1);             \
   }
+  if (dim <= 16) {
+    if (fold) PICP_LAUNCH_MM(1, 2)
+    else if (rad) PICP_LAUNCH_MM(1, 1)
+    else PICP_LAUNCH_MM(1, 0)
+  } else {
+    if (rad) PICP_LAUNCH_MM(2, 1)
+    else PICP_LAUNCH_MM(2, 0)
+  }
+#undef PICP_LAUNCH_MM3
 #undef PICP_LAUNCH_MM
   return hipGetLastError();
 }
