@@ -224,7 +224,10 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #define MM_RT 256  // reference rows per LDS tile (128: -3.4 % on C5, 512: -7 %; profiles/r01/match_ab.log)
 #endif
 #ifndef MM_BT
-#define MM_BT 4  // folded pass: column blocks whose B operands are read per LDS wait
+#define MM_BT 4  // folded pass: column blocks whose B operands are read per LDS wait (RB = 1)
+#endif
+#ifndef MM_BT2
+#define MM_BT2 4  // the same for RB = 2
 #endif
 // Diagnostic build only (-DPICP_STAMPS): [0] queries through the full-scan fallback, [1] total
 // candidates rescanned, [2] queries, [3] max candidates of a query (tools/match_stats.py).
@@ -279,6 +282,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     int xcd_map) {
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
+  constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
   constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
@@ -538,19 +542,19 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     if (more) fetch(t0 + MM_RT);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
-      // the B operands of MM_BT column blocks first (one LDS wait per group, not per block);
-      // MM_BT = 4 instead of the whole tile keeps 16 registers free for a fifth wave per SIMD
+      // the B operands of BT column blocks first (one LDS wait per group, not per block);
+      // BT = 4 instead of the whole tile keeps 16 registers free for a fifth wave per SIMD (RB = 1)
 #pragma unroll
-      for (int sg = 0; sg < MM_RT / 32; sg += MM_BT) {
-        mm_half8 bt[MM_BT];
+      for (int sg = 0; sg < MM_RT / 32; sg += BT) {
+        mm_half8 bt[BT];
 #pragma unroll
-        for (int kb = 0; kb < MM_BT; ++kb) {
+        for (int kb = 0; kb < BT; ++kb) {
           mm_half8 b1[KCH];
           load_b(buf, (sg + kb) * 32 + r, b1);
           bt[kb] = b1[0];
         }
 #pragma unroll
-        for (int kb = 0; kb < MM_BT; ++kb) {
+        for (int kb = 0; kb < BT; ++kb) {
           const int sub = sg + kb;
           const int col = sub * 32 + r;
 #pragma unroll
