@@ -657,22 +657,17 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         else if (d < second) second = d;
       }
     } else {
-      int idx[MM_CAP];
-#pragma unroll
-      for (int k = 0; k < MM_CAP; ++k) idx[k] = (k < n) ? s_list[w][lane][k] : 0x7fffffff;
-#pragma unroll
-      for (int a = 1; a < MM_CAP; ++a) {  // sort ascending (padding sorts last)
-#pragma unroll
-        for (int b = a; b > 0; --b) {
-          const int lo = min(idx[b - 1], idx[b]), hi = max(idx[b - 1], idx[b]);
-          idx[b - 1] = lo;
-          idx[b] = hi;
-        }
-      }
+      // The candidates in LDS are in no particular order (lanes append them with LDS atomics).
+      // The reference's in-order strict-'<' scan yields best = the minimum, bi = the FIRST
+      // index attaining it, second = the second smallest of the multiset; the update below
+      // yields exactly those for ANY visiting order (a tie with the best keeps the smaller
+      // index and makes second equal to best; NaN never updates; distances are sums of squares,
+      // never -0), so no sort is needed.
       for (int k = 0; k < n; ++k) {
-        const int j = idx[k];
+        const int j = s_list[w][lane][k];
         const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
         if (d < best) { second = best; best = d; bi = j; }
+        else if (d == best) { second = best; bi = min(bi, j); }
         else if (d < second) second = d;
       }
     }
