@@ -258,6 +258,12 @@ __device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t)
   return m;
 }
 
+// m = 2m + (v >= 0) for an int v (the sign bit of S' clear): compare into VCC, shift in as carry
+__device__ __forceinline__ unsigned mm_shift_in_ge0(unsigned m, int v) {
+  asm("v_cmp_le_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(m) : "v"(v) : "vcc");
+  return m;
+}
+
 // RAD = 1: the accept-only (radius) form for callers that consume only accepted[] and the
 // best_idx of accepted queries (the VO sequence): pass 1 is skipped and the candidates are the
 // references within a fixed radius of the query (mm_radius below); best_idx, best_dist and
@@ -568,9 +574,11 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
             for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
             if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
+              // the candidate mask in two instructions per element (the max tree above has
+              // already read every accumulator, so the asm is not the MFMA result's first reader)
               unsigned m = 0;
 #pragma unroll
-              for (int i = 0; i < 16; ++i) m = (m << 1) | (__float_as_int(acc[i]) >= 0 ? 1u : 0u);
+              for (int i = 0; i < 16; ++i) m = mm_shift_in_ge0(m, __float_as_int(acc[i]));
               while (m) {
                 const int i = 15 - __builtin_ctz(m);
                 m &= m - 1;
