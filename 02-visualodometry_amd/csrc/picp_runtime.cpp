@@ -922,6 +922,48 @@ static int grow(void** ptr, int64_t* cap, int64_t need, size_t elem) {
   return PICP_OK;
 }
 
+// The copy constructor of the reference's PICPSolver copies every member, including the
+// non-owning world/image pointers (src/picp_solver.h:72-81), so a copy solves the same problem.
+// Here the points live on the device: the clone gets its own copies of them, the current
+// correspondences and the pose (the cached gather is redone lazily).
+extern "C" int picp_clone(const picp_t* src, picp_t** out) {
+  CHECK_ARG(src && out, "picp_clone: null argument");
+  const picp_batch* sb = src->b;
+  picp_t* h = nullptr;
+  int rc = picp_create(&h, sb->device, sb->rows, sb->cols, sb->K);
+  if (rc) return rc;
+  memcpy(h->pose, src->pose, sizeof(h->pose));
+  auto fail = [&](int code) {
+    picp_destroy(h);
+    return code;
+  };
+  if (src->have_points) {
+    HIP_TRY(hipSetDevice(sb->device));
+    rc = grow((void**)&h->world_d, &h->cap_world, 3 * src->n_world, sizeof(float));
+    if (rc) return fail(rc);
+    rc = grow((void**)&h->image_d, &h->cap_image, 2 * src->n_image, sizeof(float));
+    if (rc) return fail(rc);
+    // the source's stream is drained first: its uploads may still be in flight
+    hipError_t e = hipStreamSynchronize(sb->stream);
+    if (e == hipSuccess && src->n_world)
+      e = hipMemcpyAsync(h->world_d, src->world_d, (size_t)src->n_world * 3 * sizeof(float),
+                         hipMemcpyDeviceToDevice, h->b->stream);
+    if (e == hipSuccess && src->n_image)
+      e = hipMemcpyAsync(h->image_d, src->image_d, (size_t)src->n_image * 2 * sizeof(float),
+                         hipMemcpyDeviceToDevice, h->b->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->b->stream);
+    if (e != hipSuccess) return fail(set_err(PICP_ERR_DEVICE, "picp_clone: %s", hipGetErrorString(e)));
+    h->n_world = src->n_world;
+    h->n_image = src->n_image;
+    h->have_points = true;
+  }
+  h->pairs_h = src->pairs_h;
+  h->m = src->m;
+  h->gathered = false;
+  *out = h;
+  return PICP_OK;
+}
+
 extern "C" int picp_set_points(picp_t* h, const float* world, int64_t n_world, const float* image,
                                int64_t n_image) {
   CHECK_ARG(h, "picp_set_points: null handle");

@@ -34,7 +34,7 @@ K_REF = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)  # src/c
 # every symbol include/picp_c.h declares (tests check the library exports all of them)
 EXPORTED = [
     "picp_params_default", "picp_abi_version", "picp_last_error", "picp_device_count",
-    "picp_create", "picp_destroy", "picp_set_camera", "picp_set_points",
+    "picp_create", "picp_destroy", "picp_set_camera", "picp_clone", "picp_set_points",
     "picp_set_correspondences", "picp_set_pose", "picp_get_pose", "picp_one_round",
     "picp_solve", "picp_linearize", "picp_batch_create", "picp_batch_destroy",
     "picp_batch_set_data", "picp_batch_set_data_device", "picp_batch_set_poses",
@@ -104,6 +104,7 @@ def lib():
         "picp_create": ([ctypes.POINTER(vp), i, i, i, fp], i),
         "picp_destroy": ([vp], i),
         "picp_set_camera": ([vp, i, i, fp], i),
+        "picp_clone": ([vp, ctypes.POINTER(vp)], i),
         "picp_set_points": ([vp, fp, i64, fp, i64], i),
         "picp_set_correspondences": ([vp, ctypes.POINTER(ctypes.c_int32), i64], i),
         "picp_set_pose": ([vp, fp], i),

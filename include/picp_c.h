@@ -78,6 +78,11 @@ int picp_device_count(int* n);
 int picp_create(picp_t** out, int device, int rows, int cols, const float K[9]);
 int picp_destroy(picp_t* h);
 int picp_set_camera(picp_t* h, int rows, int cols, const float K[9]);
+/* Replaces PICPSolver's implicit copy constructor (src/picp_solver.h:21-82: every member is
+ * copied, the world/image pointers included, so the copy keeps solving the same problem).  The
+ * new handle is on the same device with its own copies of the points, the correspondences, the
+ * camera and the pose. */
+int picp_clone(const picp_t* src, picp_t** out);
 
 /* Replaces PICPSolver::init's world/image arguments (src/picp_solver.cpp:17-23).  The
  * arrays are COPIED to device memory (the reference stores raw pointers; its icp_test

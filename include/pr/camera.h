@@ -10,6 +10,7 @@ namespace pr {
 
 class Camera {
  public:
+  EIGEN_MAKE_ALIGNED_OPERATOR_NEW
   Camera(int rows = 100, int cols = 100, const Matrix3f& camera_matrix = Matrix3f::Identity(),
          const Isometry3f& world_in_camera_pose = Isometry3f::Identity())
       : _rows(rows), _cols(cols), _camera_matrix(camera_matrix), _world_in_camera_pose(world_in_camera_pose) {}

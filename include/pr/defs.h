@@ -7,6 +7,7 @@
 // C-ABI (include/picp_c.h) reads.
 #pragma once
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -33,6 +34,11 @@ inline const float* data9(const Matrix3f& K) { return K.data(); }
 }  // namespace pr
 #else
 #define PR_HAVE_EIGEN 0
+// the reference's classes carry Eigen's aligned operator new (src/picp_solver.h:23,
+// src/camera.h:14); the POD stand-ins need no over-alignment
+#ifndef EIGEN_MAKE_ALIGNED_OPERATOR_NEW
+#define EIGEN_MAKE_ALIGNED_OPERATOR_NEW
+#endif
 namespace pr {
 
 struct Vector2f {
@@ -126,6 +132,17 @@ struct Isometry3f {
     Vector3f t = linear() * B.translation();
     C.setTranslation({t[0] + m[12], t[1] + m[13], t[2] + m[14]});
     return C;
+  }
+  // the Eigen calls the reference makes on poses (src/cam.cpp:185,220; exec/icp_test.cpp:115)
+  const Isometry3f& matrix() const { return *this; }
+  bool isApprox(const Isometry3f& o, float prec = 1e-5f) const {  // Eigen's Frobenius-norm rule
+    double d = 0, a = 0, b = 0;
+    for (int i = 0; i < 16; ++i) {
+      d += (double)(m[i] - o.m[i]) * (m[i] - o.m[i]);
+      a += (double)m[i] * m[i];
+      b += (double)o.m[i] * o.m[i];
+    }
+    return std::sqrt(d) <= prec * std::sqrt(std::min(a, b));
   }
   Isometry3f inverse() const {
     Isometry3f I;

@@ -1,12 +1,17 @@
 // pr/picp_solver.h -- drop-in pr::PICPSolver (reference: src/picp_solver.h:21-82,
 // src/picp_solver.cpp:8-105) over the C-ABI of libpicp_amd.so (include/picp_c.h).
 //
-// Same names, argument meaning and return values as the reference, so exec/icp_test.cpp
-// compiles against it unchanged (link -lpicp_amd).  Differences, all deliberate:
+// Same names, argument meaning and return values as the reference.  The reference's own sources
+// (exec/icp_test.cpp, src/cam.cpp, src/my_utilities.cpp) reach the solver through
+// `#include "picp_solver.h"` / `"camera.h"` inside src/; include/ref_src/ holds the two one-line
+// headers that replace those files, so every caller compiles against this class unchanged
+// (INTEGRATION.md §2).  Differences, all deliberate:
 //   * init() COPIES world/image points to device memory (the reference keeps raw pointers to
 //     them, src/picp_solver.cpp:21-22, and icp_test passes temporaries: use-after-free).
 //   * linearize + damped LDLT + update run on the GPU (picp_kernels.hip); oneRound() is one
 //     device round trip.  solve() runs the whole exec/icp_test.cpp:88-107 loop on the device.
+//   * copies get their own device handle with copies of the points (picp_clone); moves hand the
+//     handle over.  The reference's implicit copy shares the caller's arrays instead.
 //   * errors from the device are reported on std::cerr and make oneRound() return false;
 //     lastStatus() gives the C-ABI status code.
 // Header-only: no C++ types cross the library boundary.
@@ -22,14 +27,41 @@ namespace pr {
 
 class PICPSolver {
  public:
-  explicit PICPSolver(int device = 0) : _device(device) {
+  EIGEN_MAKE_ALIGNED_OPERATOR_NEW
+
+  //! src/picp_solver.cpp:8-15 (no handle yet: the device state is created by the first init)
+  PICPSolver() : PICPSolver(0) {}
+  explicit PICPSolver(int device) : _device(device) {
     _kernel_thereshold = 1000;  // src/picp_solver.cpp:14
     _damping = 1;               // :11
     _min_num_inliers = 0;       // :12
   }
   ~PICPSolver() { picp_destroy(_h); }
-  PICPSolver(const PICPSolver&) = delete;
-  PICPSolver& operator=(const PICPSolver&) = delete;
+
+  // Value semantics like the reference class, whose implicit copy copies every member
+  // (src/picp_solver.h:72-81); src/cam.cpp:34 assigns `picp_solver = PICPSolver();` to a by-value
+  // member.  A move hands the device handle over; a copy gets its own handle holding copies of
+  // the points, correspondences and pose (picp_clone), so it keeps solving the same problem as
+  // the reference's copy (which shares the caller's arrays) does.
+  PICPSolver(PICPSolver&& o) noexcept { take(o); }
+  PICPSolver& operator=(PICPSolver&& o) noexcept {
+    if (this != &o) {
+      picp_destroy(_h);
+      _h = nullptr;
+      take(o);
+    }
+    return *this;
+  }
+  PICPSolver(const PICPSolver& o) { copy_from(o); }
+  PICPSolver& operator=(const PICPSolver& o) {
+    if (this != &o) {
+      picp_t* keep = _h;
+      _h = nullptr;
+      copy_from(o);
+      picp_destroy(keep);
+    }
+    return *this;
+  }
 
   //! src/picp_solver.h:32-34
   void init(const Camera& camera, const Vector3fVector& world_points, const Vector2fVector& image_points) {
@@ -111,6 +143,24 @@ class PICPSolver {
   void pull_pose() {
     float T[16];
     if (picp_get_pose(_h, T) == PICP_OK) _camera.setWorldInCameraPose(iso_from16(T));
+  }
+  void copy_state(const PICPSolver& o) {
+    _device = o._device;
+    _camera = o._camera;
+    _kernel_thereshold = o._kernel_thereshold;
+    _damping = o._damping;
+    _min_num_inliers = o._min_num_inliers;
+    _stats = o._stats;
+    _status = o._status;
+  }
+  void take(PICPSolver& o) {
+    copy_state(o);
+    _h = o._h;
+    o._h = nullptr;
+  }
+  void copy_from(const PICPSolver& o) {
+    copy_state(o);
+    if (o._h) check(picp_clone(o._h, &_h), "picp_clone");
   }
 
   int _device;
