@@ -16,9 +16,12 @@
 // as hi = (float)t, lo = (float)(t - hi)), polls its S - 1 partners', and all add the parts in
 // part order: every part runs the identical solve, so no broadcast is needed.  Partners are
 // blockIdx b, b + 8, b + 16, ... which round-robin placement puts on the same XCD (speed only:
-// correctness rests on the tags).  Granules are double-buffered by round parity and zeroed by a
-// memset node before every launch; every wait has an s_memrealtime deadline, refreshed each
-// round (error word set, the problem stops, the host reports it).
+// correctness rests on the tags).  Granules are double-buffered by round parity; their tags
+// continue from per-slot tag bases the previous launch left, so the sync area is zeroed only once
+// per layout (and before the tags could wrap), not per launch.  Every wait has an s_memrealtime
+// deadline, refreshed each round (error word set, the problem stops, the host reports it and
+// re-runs the solve in graph mode).  The host launches a split grid only when the occupancy query
+// below says every block is resident at once.
 // split = 4 uses 256-thread blocks (BS = 256), two per CU from DIFFERENT problems: while one
 // problem's parts exchange and solve (the CU idle in split = 2), the other's compute; the
 // hardware issues the older block first, so the two settle into alternating phases.
@@ -279,6 +282,50 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part (BS 512)
 
+// dynamic LDS of a launch: the part of a problem (or of its 1/split share) past the
+// register-resident npt x BS items, capped by the stage
+static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out) {
+  const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
+  const int bs = (split == 4) ? 256 : PICP_BBLOCK;
+  const int lds_cap = (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
+  const int lds_items = (per_block > npt * bs) ? min(per_block - npt * bs, lds_cap) : 0;
+  if (lds_items_out) *lds_items_out = lds_items;
+  return (size_t)5 * lds_items * sizeof(float);
+}
+
+template <int N>
+static const void* block_kernel_n(bool ph, int bs) {
+  if (bs == 256) return ph ? (const void*)picp_block_kernel<N, 1, 256> : (const void*)picp_block_kernel<N, 0, 256>;
+  return ph ? (const void*)picp_block_kernel<N, 1, 512> : (const void*)picp_block_kernel<N, 0, 512>;
+}
+
+static const void* block_kernel_ptr(int npt, bool ph, int bs) {
+  switch (npt) {
+    case 1: return block_kernel_n<1>(ph, bs);
+    case 2: return block_kernel_n<2>(ph, bs);
+    case 4: return block_kernel_n<4>(ph, bs);
+    case 8: return block_kernel_n<8>(ph, bs);
+    default: return nullptr;
+  }
+}
+
+// Blocks of the variant a launch with these arguments uses that one CU holds at once (the
+// hardware limit from registers, LDS and waves; other work on the device is not counted).  The
+// host multiplies by the CU count and launches a split grid (whose blocks wait on each other)
+// only if the whole grid fits.
+extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu) {
+  if (!blocks_per_cu || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
+  const int bs = (split == 4) ? 256 : PICP_BBLOCK;
+  const void* fn = block_kernel_ptr(npt, picp_use_pinhole(K), bs);
+  if (!fn) return hipErrorInvalidValue;
+  const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr);
+  if (lds_bytes > 65536) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, bs, lds_bytes);
+}
+
 // max_n: the largest problem of the launch (sizes the LDS stage: max_n/split - npt*BS items,
 // capped).  split = 1: grid = n_problems blocks of 512.  split = 2: grid = round_up(2 n_problems,
 // 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of 256, two
@@ -294,12 +341,10 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
   if (n_problems <= 0 || !args || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
   if (split > 1 && (!xg || !err || !tagbase)) return hipErrorInvalidValue;
   const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
-  const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
   const bool ph = picp_use_pinhole(args->K);
   const int bs = (split == 4) ? 256 : PICP_BBLOCK;
-  const int lds_cap = (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
-  const int lds_items = (per_block > npt * bs) ? min(per_block - npt * bs, lds_cap) : 0;
-  const size_t lds_bytes = (size_t)5 * lds_items * sizeof(float);
+  int lds_items = 0;
+  const size_t lds_bytes = block_lds_bytes(npt, split, max_n, &lds_items);
 #define PICP_LAUNCH_B3(N, P, B)                                                                            \
   {                                                                                                        \
     if (lds_bytes > 65536)                                                                                 \

@@ -325,6 +325,22 @@ extern "C" hipError_t picp_debug_pstamps(unsigned long long* out, size_t n_words
 // ------------------------------- host launch wrapper -------------------------------
 extern "C" int picp_persistent_block(void) { return PICP_PBLOCK; }
 
+// Blocks of the persistent variant for (npt, K) one CU holds at once (registers, LDS, waves).
+// Its blocks hand rounds to each other, so the host launches it only when grid <= this x CUs.
+extern "C" hipError_t picp_persistent_occupancy(int npt, const float K[9], int* blocks_per_cu) {
+  if (!blocks_per_cu) return hipErrorInvalidValue;
+  const bool ph = picp_use_pinhole(K);
+  const void* fn = nullptr;
+  switch (npt) {
+    case 1: fn = ph ? (const void*)picp_persistent_kernel<1, 1> : (const void*)picp_persistent_kernel<1, 0>; break;
+    case 2: fn = ph ? (const void*)picp_persistent_kernel<2, 1> : (const void*)picp_persistent_kernel<2, 0>; break;
+    case 4: fn = ph ? (const void*)picp_persistent_kernel<4, 1> : (const void*)picp_persistent_kernel<4, 0>; break;
+    case 8: fn = ph ? (const void*)picp_persistent_kernel<8, 1> : (const void*)picp_persistent_kernel<8, 0>; break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, PICP_PBLOCK, 0);
+}
+
 extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int npt, const float* X,
                                              const float* Y, const float* Z, const float* U,
                                              const float* V, const PicpArgs* args,

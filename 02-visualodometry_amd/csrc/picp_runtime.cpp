@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "picp_c.h"
+#include "picp_comm.h"
 #include "picp_host.h"
 #include "picp_internal.h"
 
@@ -43,6 +44,8 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         unsigned int* tagbase, unsigned long long timeout_ticks);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_persistent_block(void);
+extern "C" hipError_t picp_persistent_occupancy(int npt, const float K[9], int* blocks_per_cu);
+extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu);
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,
                                         const float* q_desc, const float* r_desc,
                                         const MatchProblem* probs, int dim, float dist_thr,
@@ -198,6 +201,11 @@ struct picp_batch {
   int result_idx = 0;          // st_d[] holding the final state of the last solve
   bool last_persistent = false;  // the last solve was a persistent launch (check its error word)
   unsigned long long timeout_ticks = 20000000ull;  // 200 ms of s_memrealtime (100 MHz)
+  // co-residency (persistent and split block modes hand rounds between blocks of one launch)
+  bool no_handoff = false;     // a hand-off wait timed out once: lay out without cross-block waits
+  int fallbacks = 0;           // solves re-run in graph mode after a timed-out hand-off
+  int handoff_grid = 0;        // blocks of the hand-off launch (0: the mode has none)
+  int handoff_resident = 0;    // blocks the device holds at once for it (occupancy x CUs)
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -250,8 +258,19 @@ static int items_per_block(int64_t total, int num_cu) {
   return (int)round_up((total + nb - 1) / nb, 4);
 }
 
+// Resident blocks per CU for a hand-off launch: the occupancy query of the exact kernel variant,
+// capped by PICP_RESIDENT_BLOCKS_PER_CU (a test hook that emulates a device partly held by other
+// work; 0 forces the layouts without cross-block waits).
+static int resident_per_cu(hipError_t q, int occ) {
+  if (q != hipSuccess) occ = 0;
+  if (const char* e = getenv("PICP_RESIDENT_BLOCKS_PER_CU")) occ = std::min(occ, std::max(0, atoi(e)));
+  return occ;
+}
+
 // (Re)build the partition for correspondence offsets `offs` (np+1 entries).
-static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
+static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
+  const std::vector<int64_t> offs_copy(offs_in, offs_in + np + 1);  // offs_in may be b->offs itself
+  const int64_t* offs = offs_copy.data();
   CHECK_ARG(np >= 1, "batch: n_problems must be >= 1");
   for (int i = 0; i < np; ++i)
     CHECK_ARG(offs[i + 1] >= offs[i] && offs[0] == 0, "batch: corr_offsets must be a prefix sum from 0");
@@ -305,7 +324,19 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
         }
       }
     }
-    (void)pnb;
+    // Persistent blocks wait on each other every round, so all of them must be resident at once:
+    // launch that mode only when the occupancy query says the grid fits (otherwise, or after a
+    // timed-out hand-off, the batch runs in graph mode).
+    b->handoff_grid = 0;
+    b->handoff_resident = 0;
+    if (pnpt && b->no_handoff) pnpt = 0;
+    if (pnpt) {
+      int occ = 0;
+      const int res = resident_per_cu(picp_persistent_occupancy(pnpt, b->K, &occ), occ) * b->num_cu;
+      b->handoff_grid = pnb * np;
+      b->handoff_resident = res;
+      if ((int64_t)pnb * np > res) pnpt = 0;
+    }
     if (force_graph) {
       b->mode = PICP_MODE_GRAPH;
     } else if (force_block && bnpt) {
@@ -327,6 +358,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
       // PICP_BLOCK_SPLIT=1|2 forces
       auto grid_of = [&](int s) { return ((s * np + 8 * s - 1) / (8 * s)) * (8 * s); };
       int split = (grid_of(2) <= b->num_cu && max_n >= 4096) ? 2 : 1;
+      if (b->no_handoff) split = 1;
       // (split 4 -- four 256-thread parts per problem, two blocks per CU from different
       // problems, meant to overlap one problem's exchange + solve with the other's linearize --
       // measured 5 % slower than split 2 at C4 (profiles/r01/c4_split4_ab.log): PICP_BLOCK_SPLIT=4)
@@ -335,6 +367,23 @@ static int batch_layout(picp_batch* b, const int64_t* offs, int np) {
         if (v == 1) split = 1;
         if (v == 2 && grid_of(2) <= b->num_cu) split = 2;
         if (v == 4 && grid_of(4) <= 2 * b->num_cu) split = 4;
+        if (b->no_handoff) split = 1;
+      }
+      // the parts of a split problem wait on each other every round: keep the split only if the
+      // occupancy query says the whole grid is resident at once
+      while (split > 1) {
+        const int64_t part = round_up((max_n + split - 1) / split, 4);
+        const int bs = (split == 4) ? 256 : 512;
+        int cap = picp_block_max_items() / 512;
+        if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
+        int snpt = 1;
+        while (snpt < cap && (int64_t)snpt * bs < part) snpt *= 2;
+        int occ = 0;
+        const int res = resident_per_cu(picp_block_occupancy(snpt, split, (int)max_n, b->K, &occ), occ) * b->num_cu;
+        b->handoff_grid = grid_of(split);
+        b->handoff_resident = res;
+        if (grid_of(split) <= res) break;
+        split = (split == 4) ? 2 : 1;
       }
       b->split = split;
       if (split > 1) {  // register items per lane for a part
@@ -594,15 +643,57 @@ static hipError_t persistent_tag_guard(picp_batch* b, int R, int solves) {
   return hipSuccess;
 }
 
+// Enqueue one fused solve.  Persistent and block modes are ONE kernel launch: it goes to the
+// stream directly (back-to-back launches queue behind each other with only the kernel-boundary
+// gap; a one-node graph replay measured ~10 us more per solve).  Graph mode replays the captured
+// prologue + R round launches.
+static int enqueue_fused(picp_batch* b, int R) {
+  if (b->mode == PICP_MODE_GRAPH) {
+    int rc = ensure_graph(b, R);
+    if (rc) return rc;
+    HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
+  } else {
+    HIP_TRY(enqueue_solve(b, R));
+  }
+  return PICP_OK;
+}
+
 static int batch_solve_async(picp_batch* b, const picp_params* prm) {
   HIP_TRY(hipSetDevice(b->device));
   int rc = batch_upload_params(b, prm);
   if (rc) return rc;
   const int R = prm->max_rounds;
-  rc = ensure_graph(b, R);
-  if (rc) return rc;
   HIP_TRY(persistent_tag_guard(b, R, 1));
-  HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
+  rc = enqueue_fused(b, R);
+  if (rc) return rc;
+  b->last_rounds = R;
+  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
+  b->last_persistent = uses_err_word(b);
+  return PICP_OK;
+}
+
+static int batch_layout(picp_batch* b, const int64_t* offs_in, int np);
+
+// A cross-block hand-off wait timed out (the blocks were not all resident: another process or
+// stream held CUs, or the device time-sliced the launch).  Lay the batch out again without
+// hand-offs (persistent -> graph mode, split block -> one block per problem), keep its data and
+// initial poses, and re-run the same solve; later solves keep that layout.
+static int batch_rerun_without_handoff(picp_batch* b) {
+  const std::vector<PicpState> init = b->init_h;
+  const picp_params prm = b->params;
+  const int R = b->last_rounds;
+  b->no_handoff = true;
+  b->fallbacks++;
+  int rc = batch_layout(b, b->offs.data(), b->np);
+  if (rc) return rc;
+  b->init_h = init;
+  HIP_TRY(hipMemcpyAsync(b->init_d, b->init_h.data(), (size_t)b->np * sizeof(PicpState), hipMemcpyHostToDevice, b->stream));
+  picp_params p2 = prm;
+  p2.max_rounds = R;
+  rc = batch_upload_params(b, &p2);
+  if (rc) return rc;
+  rc = enqueue_fused(b, R);
+  if (rc) return rc;
   b->last_rounds = R;
   b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
   b->last_persistent = uses_err_word(b);
@@ -623,7 +714,11 @@ static int batch_read_results(picp_batch* b) {
     HIP_TRY(hipMemsetAsync(b->sync, 0, b->sync_bytes, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->tag_rounds = 0;
-    return set_err(PICP_ERR_DEVICE, "solve: a cross-block hand-off wait timed out (code %u)", err);
+    if (b->no_handoff)  // cannot happen: that layout has no cross-block waits
+      return set_err(PICP_ERR_DEVICE, "solve: a cross-block hand-off wait timed out (code %u)", err);
+    int rc = batch_rerun_without_handoff(b);
+    if (rc) return rc;
+    return batch_read_results(b);
   }
   return PICP_OK;
 }
@@ -773,81 +868,144 @@ extern "C" int picp_batch_info(picp_batch_t* b, int64_t* total, int* nblk, int* 
   return PICP_OK;
 }
 
+// hipEvents destroyed on every return path
+struct EventPair {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipError_t create() {
+    hipError_t e = hipEventCreate(&a);
+    return e == hipSuccess ? hipEventCreate(&b) : e;
+  }
+  ~EventPair() {
+    if (a) hipEventDestroy(a);
+    if (b) hipEventDestroy(b);
+  }
+};
+
 extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps,
-                               float* total_ms, float kernel_us[2]) {
+                               float* total_ms, float* launch_us) {
   CHECK_ARG(b && prm && reps > 0, "picp_batch_time: bad argument");
   HIP_TRY(hipSetDevice(b->device));
   int rc = batch_upload_params(b, prm);
   if (rc) return rc;
   const int R = prm->max_rounds;
-  rc = ensure_graph(b, R);
-  if (rc) return rc;
-  hipEvent_t e0, e1;
-  HIP_TRY(hipEventCreate(&e0));
-  HIP_TRY(hipEventCreate(&e1));
-  HIP_TRY(persistent_tag_guard(b, R, reps + 1));  // the timed replays and the event-pair solve
-  HIP_TRY(hipEventRecord(e0, b->stream));
-  for (int r = 0; r < reps; ++r) HIP_TRY(hipGraphLaunch(b->gexec, b->stream));
-  HIP_TRY(hipEventRecord(e1, b->stream));
-  HIP_TRY(hipEventSynchronize(e1));
+  if (b->mode == PICP_MODE_GRAPH) {
+    rc = ensure_graph(b, R);  // captured before the timed region
+    if (rc) return rc;
+  }
+  EventPair ev;
+  HIP_TRY(ev.create());
+  HIP_TRY(persistent_tag_guard(b, R, reps));
+  HIP_TRY(hipEventRecord(ev.a, b->stream));
+  for (int r = 0; r < reps; ++r) {
+    rc = enqueue_fused(b, R);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(ev.b, b->stream));
+  HIP_TRY(hipEventSynchronize(ev.b));
   float ms = 0.0f;
-  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
   if (total_ms) *total_ms = ms;
   b->last_rounds = R;
   b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
   b->last_persistent = uses_err_word(b);
-  if (kernel_us) {
-    // [0]: mean launch period of the round kernel inside the replayed graphs (event time over
-    //      the timed replays / kernel launches; the graphs are back-to-back launches, so this is
-    //      the per-launch duration a kernel trace reports);
-    // [1]: mean of event pairs around single launches of the same solve (an upper bound: it
-    //      adds the event overhead to every launch).
-    const int launches = (b->mode == PICP_MODE_GRAPH) ? std::max(R, 1) : 1;
-    kernel_us[0] = 1000.0f * ms / (float)(reps * launches);
-    if (b->mode != PICP_MODE_GRAPH) {
-      hipEvent_t a0, a1;
-      HIP_TRY(hipEventCreate(&a0));
-      HIP_TRY(hipEventCreate(&a1));
-      HIP_TRY(hipEventRecord(a0, b->stream));
-      HIP_TRY(enqueue_solve(b, R));
-      HIP_TRY(hipEventRecord(a1, b->stream));
-      HIP_TRY(hipEventSynchronize(a1));
-      float t = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&t, a0, a1));
-      kernel_us[1] = 1000.0f * t;
-      hipEventDestroy(a0);
-      hipEventDestroy(a1);
-      hipEventDestroy(e0);
-      hipEventDestroy(e1);
-      b->result_idx = 0;
-      b->last_persistent = uses_err_word(b);
-      return batch_read_results(b);
-    }
-    std::vector<hipEvent_t> ev((size_t)(R + 1));
-    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
-    double lin_us = 0.0;
-    int lin_n = 0;
-    HIP_TRY(graph_prologue(b));
-    for (int j = 0; j < R; ++j) {
-      HIP_TRY(hipEventRecord(ev[j], b->stream));
-      HIP_TRY(launch_round(b, j));
-    }
-    HIP_TRY(hipEventRecord(ev[R], b->stream));
-    HIP_TRY(hipEventSynchronize(ev[R]));
-    for (int j = 0; j < R; ++j) {
-      float t = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&t, ev[j], ev[j + 1]));
-      lin_us += 1000.0 * t;
-      ++lin_n;
-    }
-    for (auto& e : ev) hipEventDestroy(e);
-    kernel_us[1] = lin_n ? (float)(lin_us / lin_n) : 0.0f;
-    b->result_idx = graph_result_idx(R);
-    b->last_persistent = false;
-  }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  // mean launch period of the dominant kernel inside the region (graph mode: R round launches
+  // per solve; otherwise one launch per solve); back-to-back launches, so this is the per-launch
+  // duration a kernel trace reports plus the boundary gap
+  const int launches = (b->mode == PICP_MODE_GRAPH) ? std::max(R, 1) : 1;
+  if (launch_us) *launch_us = 1000.0f * ms / (float)(reps * launches);
   return batch_read_results(b);
+}
+
+extern "C" int picp_batch_time_single(picp_batch_t* b, const picp_params* prm, float* us) {
+  CHECK_ARG(b && prm && us, "picp_batch_time_single: bad argument");
+  HIP_TRY(hipSetDevice(b->device));
+  int rc = batch_upload_params(b, prm);
+  if (rc) return rc;
+  const int R = prm->max_rounds;
+  HIP_TRY(persistent_tag_guard(b, R, 1));
+  if (b->mode != PICP_MODE_GRAPH) {
+    EventPair ev;
+    HIP_TRY(ev.create());
+    HIP_TRY(hipEventRecord(ev.a, b->stream));
+    HIP_TRY(enqueue_solve(b, R));
+    HIP_TRY(hipEventRecord(ev.b, b->stream));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    float t = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&t, ev.a, ev.b));
+    *us = 1000.0f * t;
+    b->last_rounds = R;
+    b->result_idx = 0;
+    b->last_persistent = uses_err_word(b);
+    return batch_read_results(b);
+  }
+  std::vector<EventPair> ev((size_t)std::max(R, 1));
+  for (auto& e : ev) HIP_TRY(e.create());
+  HIP_TRY(graph_prologue(b));
+  for (int j = 0; j < R; ++j) {
+    HIP_TRY(hipEventRecord(ev[j].a, b->stream));
+    HIP_TRY(launch_round(b, j));
+    HIP_TRY(hipEventRecord(ev[j].b, b->stream));
+  }
+  if (R > 0) HIP_TRY(hipEventSynchronize(ev[R - 1].b));
+  double sum = 0.0;
+  for (int j = 0; j < R; ++j) {
+    float t = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&t, ev[j].a, ev[j].b));
+    sum += 1000.0 * t;
+  }
+  *us = R > 0 ? (float)(sum / R) : 0.0f;
+  b->last_rounds = R;
+  b->result_idx = graph_result_idx(R);
+  b->last_persistent = false;
+  return batch_read_results(b);
+}
+
+extern "C" int picp_batch_residency(picp_batch_t* b, int* grid, int* resident, int* fallbacks) {
+  CHECK_ARG(b, "picp_batch_residency: null batch");
+  if (grid) *grid = b->handoff_grid;
+  if (resident) *resident = b->handoff_resident;
+  if (fallbacks) *fallbacks = b->fallbacks;
+  return PICP_OK;
+}
+
+// Gather every rank's results of the batch split: this rank's batch holds the
+// problems picp_shard_range(n_total, world, rank) gives it; after its solve, one RCCL all-gather
+// of the 128-B per-problem states (on the batch's stream, device to device over xGMI) and one
+// copy to the host give every rank all n_total poses and stats in problem order.
+extern "C" int picp_batch_allgather(picp_batch_t* b, picp_comm_t* c, int64_t n_total, float* T_all,
+                                    picp_stats* st_all) {
+  CHECK_ARG(b && c && T_all, "picp_batch_allgather: null argument");
+  CHECK_ARG(picp_comm_device(c) == b->device, "picp_batch_allgather: communicator and batch are on different devices");
+  const int world = picp_comm_world(c), rank = picp_comm_rank(c);
+  int64_t f0 = 0, f1 = 0;
+  int rc = picp_shard_range(n_total, world, rank, &f0, &f1);
+  if (rc) return rc;
+  CHECK_ARG(f1 - f0 == b->np, "picp_batch_allgather: the batch does not hold this rank's shard of n_total");
+  HIP_TRY(hipSetDevice(b->device));
+  rc = batch_read_results(b);  // the solve is complete (re-run if a hand-off timed out)
+  if (rc) return rc;
+  const int64_t maxn = (n_total + world - 1) / world;
+  const size_t bytes = (size_t)std::max<int64_t>(maxn, 1) * sizeof(PicpState);
+  void* send = picp_comm_send_buffer(c, bytes);
+  if (!send) return set_err(PICP_ERR_NOMEM, "picp_batch_allgather: staging buffer of %zu B", bytes);
+  HIP_TRY(hipMemcpyAsync(send, b->st_d[b->result_idx], (size_t)b->np * sizeof(PicpState), hipMemcpyDeviceToDevice,
+                         b->stream));
+  const void* recv = nullptr;
+  rc = picp_comm_allgather_dev(c, send, bytes, b->stream, &recv);
+  if (rc) return rc;
+  std::vector<PicpState> all((size_t)world * std::max<int64_t>(maxn, 1));
+  HIP_TRY(hipMemcpyAsync(all.data(), recv, all.size() * sizeof(PicpState), hipMemcpyDeviceToHost, b->stream));
+  HIP_TRY(hipStreamSynchronize(b->stream));
+  for (int r = 0; r < world; ++r) {
+    int64_t a = 0, e = 0;
+    picp_shard_range(n_total, world, r, &a, &e);
+    for (int64_t k = 0; k < e - a; ++k) {
+      const PicpState& st = all[(size_t)r * maxn + k];
+      state_to_pose(st, T_all + 16 * (a + k));
+      if (st_all) state_to_stats(st, st_all[a + k]);
+    }
+  }
+  return PICP_OK;
 }
 
 // ------------------------------------------------------------------------------------

@@ -39,12 +39,16 @@ EXPORTED = [
     "picp_solve", "picp_linearize", "picp_batch_create", "picp_batch_destroy",
     "picp_batch_set_data", "picp_batch_set_data_device", "picp_batch_set_poses",
     "picp_batch_get_poses", "picp_batch_get_stats", "picp_batch_solve",
-    "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_info",
+    "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_time_single",
+    "picp_batch_info", "picp_batch_residency",
     "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
     "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async",
     "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
     "picp_vo_info", "picp_selftest_rcp", "picp_essential_params_default", "picp_essential_batch",
+    "picp_shard_range", "picp_comm_unique_id", "picp_comm_create", "picp_comm_destroy", "picp_comm_info",
+    "picp_comm_allreduce_max", "picp_comm_barrier", "picp_batch_allgather",
 ]
+COMM_ID_BYTES = 128
 
 
 class PicpError(RuntimeError):
@@ -123,6 +127,8 @@ def lib():
         "picp_batch_solve_async": ([vp, pp], i),
         "picp_batch_sync": ([vp], i),
         "picp_batch_time": ([vp, pp, i, fp, fp], i),
+        "picp_batch_time_single": ([vp, pp, fp], i),
+        "picp_batch_residency": ([vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "picp_batch_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         "picp_triangulate": ([i, fp, fp, fp, fp, i64, fp], i),
         "picp_projection_matrix": ([fp, fp, fp], i),
@@ -142,6 +148,14 @@ def lib():
         "picp_vo_time": ([vp, i, fp], i),
         "picp_selftest_rcp": ([i, i, i, ctypes.POINTER(ctypes.c_uint64)], i),
         "picp_vo_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i)], i),
+        "picp_shard_range": ([i64, i, i, ctypes.POINTER(i64), ctypes.POINTER(i64)], i),
+        "picp_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], i),
+        "picp_comm_create": ([ctypes.POINTER(vp), i, i, i, ctypes.POINTER(ctypes.c_uint8)], i),
+        "picp_comm_destroy": ([vp], i),
+        "picp_comm_info": ([vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)], i),
+        "picp_comm_allreduce_max": ([vp, dp, i], i),
+        "picp_comm_barrier": ([vp], i),
+        "picp_batch_allgather": ([vp, vp, i64, fp, sp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -346,11 +360,24 @@ class Batch:
         _check(lib().picp_batch_sync(self._b))
 
     def time(self, reps, **params):
+        """reps back-to-back solves between two HIP events -> (total ms, mean launch period us)."""
         prm = default_params(**params)
         total = ctypes.c_float(0)
-        kus = (ctypes.c_float * 2)()
-        _check(lib().picp_batch_time(self._b, ctypes.byref(prm), reps, ctypes.byref(total), kus))
-        return total.value, (kus[0], kus[1])
+        lus = ctypes.c_float(0)
+        _check(lib().picp_batch_time(self._b, ctypes.byref(prm), reps, ctypes.byref(total), ctypes.byref(lus)))
+        return total.value, lus.value
+
+    def time_single(self, **params):
+        """Diagnostic: event pair around each launch of one solve (us; graph mode: per round)."""
+        prm = default_params(**params)
+        us = ctypes.c_float(0)
+        _check(lib().picp_batch_time_single(self._b, ctypes.byref(prm), ctypes.byref(us)))
+        return us.value
+
+    def residency(self):
+        g, r, f = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().picp_batch_residency(self._b, ctypes.byref(g), ctypes.byref(r), ctypes.byref(f)))
+        return {"handoff_grid": g.value, "resident_blocks": r.value, "fallbacks": f.value}
 
     def info(self):
         tot = ctypes.c_int64(0)
@@ -359,6 +386,57 @@ class Batch:
         _check(lib().picp_batch_info(self._b, ctypes.byref(tot), ctypes.byref(nb), ctypes.byref(mode)))
         return {"total_corr": tot.value, "n_blocks": nb.value,
                 "mode": {0: "graph", 1: "persistent", 2: "block"}[mode.value]}
+
+
+def shard_range(n_items, world, rank):
+    """picp_shard_range: the contiguous [first, last) of n_items that rank owns."""
+    a, e = ctypes.c_int64(0), ctypes.c_int64(0)
+    _check(lib().picp_shard_range(n_items, world, rank, ctypes.byref(a), ctypes.byref(e)))
+    return a.value, e.value
+
+
+def comm_unique_id():
+    """RCCL unique id (bytes) for Comm; rank 0 makes it, the launcher passes it to every rank."""
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    _check(lib().picp_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """picp_comm_t: this rank's RCCL communicator of the batch split, driven by the C++ library."""
+
+    def __init__(self, device, world, rank, uid):
+        assert len(uid) == COMM_ID_BYTES
+        self._c = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        _check(lib().picp_comm_create(ctypes.byref(self._c), device, world, rank, buf))
+        self.device, self.world, self.rank = device, world, rank
+
+    def close(self):
+        if self._c:
+            lib().picp_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def allreduce_max(self, values):
+        v = np.ascontiguousarray(values, np.float64).reshape(-1).copy()
+        _check(lib().picp_comm_allreduce_max(self._c, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), v.size))
+        return v
+
+    def barrier(self):
+        _check(lib().picp_comm_barrier(self._c))
+
+    def allgather_batch(self, batch, n_total):
+        """Every rank's poses (n_total, 4, 4) and stats dicts, after this rank's batch solve."""
+        T = np.zeros(16 * n_total, np.float32)
+        st = (Stats * max(n_total, 1))()
+        _check(lib().picp_batch_allgather(batch._b, self._c, n_total, _fptr(T), st))
+        return np.transpose(T.reshape(n_total, 4, 4), (0, 2, 1)).copy(), [st[k].as_dict() for k in range(n_total)]
 
 
 def projection_matrix(K, T_cw):

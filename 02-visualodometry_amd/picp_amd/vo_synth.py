@@ -96,9 +96,21 @@ class VOSequence:
         ids = (k - self._k0) * n + np.arange(n, dtype=np.int64)
         return ids, xyz, desc
 
-    def frame(self, k):
-        """Observations of frame k: dict(uv f32 (m,2), desc f32 (m,10), id_real i64, id_meas i32)."""
-        parts = [self.landmarks(j) for j in range(max(k - 3, self._k0), k + 30)]
+    def frame(self, k, cache=None):
+        """Observations of frame k: dict(uv f32 (m,2), desc f32 (m,10), id_real i64, id_meas i32).
+        cache: optional dict step -> landmarks(step), shared by consecutive frames (each frame
+        sees 33 spawn steps, so a range of frames reuses them; the values are the same)."""
+        js = range(max(k - 3, self._k0), k + 30)
+        if cache is None:
+            parts = [self.landmarks(j) for j in js]
+        else:
+            for j in [j for j in cache if j < js[0]]:
+                del cache[j]
+            parts = []
+            for j in js:
+                if j not in cache:
+                    cache[j] = self.landmarks(j)
+                parts.append(cache[j])
         ids = np.concatenate([p[0] for p in parts])
         xyz = np.concatenate([p[1] for p in parts])
         desc = np.concatenate([p[2] for p in parts])
@@ -116,7 +128,8 @@ class VOSequence:
 
     def frames(self, k0, k1):
         """Frames [k0, k1) packed: dict(frame_off int64 (n+1), uv, desc, id_real, T_cw (n,4,4) f32)."""
-        fs = [self.frame(k) for k in range(k0, k1)]
+        cache = {}
+        fs = [self.frame(k, cache) for k in range(k0, k1)]
         off = np.zeros(len(fs) + 1, np.int64)
         off[1:] = np.cumsum([len(f["uv"]) for f in fs])
         return {"frame_off": off,

@@ -1,28 +1,43 @@
 #!/usr/bin/env python3
 """PICP hot-path benchmark (BASELINE.json metric: PICP iterations/sec @ N correspondences).
 
-Default workload (N=1): BASELINE configs[1] = C2, a single synthetic frame with 100,000
-3D<->2D correspondences, 50 Gauss-Newton rounds (convergence test disabled for timing), on one
-MI355X.  One "step" = one full 50-round solve of the frame (inputs resident in HBM, one hipGraph
-replay: initial-state copy + 50 linearize launches + 1 finalize launch).  value = rounds
-executed by all ranks / max-over-ranks wall time of the timed region.
+Headline (every N): BASELINE configs[1] = C2 on each GPU -- one synthetic frame of 100,000
+3D<->2D correspondences per GPU, 50 Gauss-Newton rounds (convergence test disabled for timing).
+One "step" = one full 50-round solve of the frame (inputs resident in HBM; one persistent
+launch).  value = rounds executed by all ranks / max-over-ranks wall time of the timed region
+(weak scaling: every rank solves its own independent frame, seed 42 + rank).
 
-Multi-GPU (torchrun, one process per GPU): every rank solves its own independent frame
-(seed 42 + rank) -> weak scaling, no data-path collective; rank 0 gathers the final poses once
-after timing (RCCL all_gather) to check them.
+Multi-GPU: `python bench.py --gpus N` (no WORLD_SIZE in the environment) starts N child processes
+itself (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE set, never exec) and relays rank 0's line; under
+torchrun the process is already one rank.  The ranks share a gloo group (CPU, only to hand the
+RCCL unique id around); every collective of the measurement -- the barriers, the max over ranks
+of the timed region, the all-gather of the C4 results -- is RCCL over xGMI driven by the C++
+library (picp_comm_*, include/picp_c.h).
+
+Sub-results on the same line (default run, bounded time):
+  c4 : BASELINE configs[3]: 1024 independent frames x 10k correspondences, sharded across the N
+       GPUs (strong scaling of the fixed batch: each rank solves picp_shard_range's frames; the
+       timed region ends with one RCCL all-gather of all 1024 poses + stats).
+  c3 : configs[2] (N = 1 only): one 1M-correspondence frame, 30 % outliers, chi2 gate.
+  c5 : configs[4]: the 10k-frame synthetic VO sequence, contiguous segments split over ranks.
+Each carries value, ms_per_step, the dominant kernel's launch time, its committed PMC traffic
+(profiles/) and, at N = 1, the oracle's CPU baseline on a bounded sample.
 
 Printed JSON also carries:
-  roofline     : the dominant kernel of the chosen execution mode (persistent: the whole 50-round
-                 solve in one launch; graph: one launch per round); achieved = 20 algorithmic bytes
-                 per correspondence-round (x,y,z,u,v float32 SoA) x correspondence-rounds per launch
-                 / mean launch duration, the duration from HIP events around the timed replays on
-                 the library's stream.
+  roofline     : the dominant kernel of the headline (picp_persistent_kernel: the whole 50-round
+                 solve in one launch); achieved = 20 algorithmic bytes per correspondence-round
+                 (x,y,z,u,v float32 SoA) x correspondence-rounds per launch / mean launch period,
+                 the period from HIP events around the timed launches on the library's stream.
+                 roofline.latency: the same kernel against its per-round latency floor (C2 is a
+                 hand-off-latency-bound kernel).
   cpu_baseline : the oracle's faithful float32 single-thread restatement (kind "port"), timed on
                  this host on a bounded sample of the same workload.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,13 +47,96 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_CORR = 20    # x,y,z,u,v float32 per correspondence-round
+HANDOFF_US = 0.8       # MI355X_MICROARCH.md price list, handoff-1to1 (idle, 8-B granule)
 
 WORKLOADS = {
     "c2": dict(n=100000, problems=1, outlier=0.0, desc="C2 single-frame PICP, 100k synthetic correspondences, 50 GN rounds"),
     "c3": dict(n=1000000, problems=1, outlier=0.3, desc="C3 single-frame PICP, 1M synthetic correspondences, 30% outliers + chi2 rejection, 50 GN rounds"),
-    "c4": dict(n=10000, problems=128, outlier=0.0, desc="C4 batch of independent frames x 10k correspondences (128 per GPU), 50 GN rounds each"),
+    "c4": dict(n=10000, problems=1024, outlier=0.0, desc="C4 batch of 1024 independent frames x 10k correspondences, sharded across the GPUs, 50 GN rounds each"),
     "c5": dict(frames=10000, obs=2000, desc="C5 full VO pipeline: 10k-frame synthetic sequence, per frame match -> PICP -> match -> triangulate on GPU, frame-parallel segments"),
 }
+THRESHOLD = 3000.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` outside torchrun: N fresh child processes, one per GPU (subprocess,
+    never exec; this parent never touches the GPU).  Rank 0's stdout is the bench line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        for p in procs:
+            p.wait()
+            if p.returncode != 0 and rc == 0:
+                rc = p.returncode
+                for q in procs:  # one rank failed: the others would block in a collective
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc if rc >= 0 else 1
+
+
+class Ranks:
+    """This process's place in the job: world/rank, the gloo group (CPU; the RCCL unique id and
+    plan-only gathers) and the RCCL communicator of the C++ library (GPU runs)."""
+
+    def __init__(self, plan_only):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.comm = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+        if not plan_only and self.world > 1:
+            import picp_amd
+            uid = [picp_amd.comm_unique_id() if self.rank == 0 else None]
+            self.dist.broadcast_object_list(uid, src=0)
+            self.comm = picp_amd.Comm(self.local, self.world, self.rank, uid[0])
+
+    @property
+    def device(self):
+        return self.local if self.world > 1 else 0
+
+    def barrier(self):
+        if self.comm is not None:
+            self.comm.barrier()
+
+    def max(self, values):
+        if self.comm is None:
+            return list(values)
+        return list(self.comm.allreduce_max(values))
+
+    def gather_obj(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+        if self.dist is not None:
+            self.dist.destroy_process_group()
 
 
 def main():
@@ -49,113 +147,132 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--n", type=int, default=0, help="override correspondences per frame")
-    ap.add_argument("--problems", type=int, default=0, help="override frames per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--problems", type=int, default=0, help="override frames (c4: total over ranks)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (headline)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--skip-extras", action="store_true",
-                    help="only the timed solves (profiling runs: no convergence-enabled re-solve)")
+                    help="only the timed solves (profiling runs: no sub-results, no side measurements)")
     ap.add_argument("--frames", type=int, default=0, help="c5: sequence length (default 10000)")
     ap.add_argument("--obs", type=int, default=0, help="c5: observations per frame (default 2000)")
     ap.add_argument("--seg-len", type=int, default=40, help="c5: PICP steps per segment")
     ap.add_argument("--stream-n", type=int, default=16000000,
                     help="c2: also measure one streaming single frame of this many correspondences "
                          "(roofline_streaming; 0 = skip)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="no GPU: start the ranks, shard every workload, gather the partition (CPU test)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
-    import torch  # plumbing only: process group, barrier, device sync (loaded before the HIP lib)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
+    rk = Ranks(args.plan_only)
+    try:
+        if args.plan_only:
+            return plan_only(args, rk)
+        import torch  # plumbing only: device sync around the timed region
+        if torch.cuda.is_available():
+            torch.cuda.set_device(rk.device)
+        if args.workload == "c5":
+            out = bench_vo(args, rk, torch)
+        elif args.workload == "c4":
+            out = bench_c4(args, rk, torch)
+        else:
+            out = bench_frame(args, rk, torch)
+        if rk.rank == 0:
+            print(json.dumps(out), flush=True)
+    finally:
+        rk.close()
+
+
+def _sync(torch):
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def pmc_traffic(name, fetch_scale=2.0):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC passes of the same command
+    (profiles/rNN/<name>_pmc_{FETCH_SIZE,WRITE_SIZE}.json, written by tools/gpu_pmc*.sh from two
+    separate --pmc passes).  FETCH_SIZE x fetch_scale (gfx950: x2 for wide coalesced streams,
+    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB.  (None, None) when absent: bench.py
+    cannot collect PMC counters live."""
+    import glob
+    dirs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*")))
+    for d in reversed(dirs):
+        f, w = (os.path.join(d, "%s_pmc_%s.json" % (name, c)) for c in ("FETCH_SIZE", "WRITE_SIZE"))
+        if os.path.exists(f) and os.path.exists(w):
+            fk = json.load(open(f))["FETCH_SIZE"]["mean"]
+            wk = json.load(open(w))["WRITE_SIZE"]["mean"]
+            src = "%s (FETCH_SIZE %.1f KiB x %g + WRITE_SIZE %.1f KiB per launch)" % (
+                os.path.relpath(f, ROOT).replace("FETCH_SIZE", "{FETCH,WRITE}_SIZE"), fk, fetch_scale, wk)
+            return round((fk * fetch_scale + wk) * 1024.0), src
+    return None, None
+
+
+def _kernel_name(mode):
+    return {"graph": "picp_round_kernel (one GN round per launch)",
+            "persistent": "picp_persistent_kernel (all GN rounds in one launch)",
+            "block": "picp_block_kernel (all GN rounds, one block per frame)"}[mode]
+
+
+def _roofline(b, R, launch_us, pmc_name):
+    """Roofline of the batch's dominant kernel from the mean launch period of the timed region."""
+    info = b.info()
+    corr_per_launch = int(info["total_corr"]) * (1 if info["mode"] == "graph" else R)
+    per_launch = BYTES_PER_CORR * corr_per_launch
+    achieved = per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
+    traffic, tsrc = pmc_traffic(pmc_name) if pmc_name else (None, None)
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
+            "kernel": _kernel_name(info["mode"]), "mode": info["mode"], "kernel_us": round(launch_us, 3),
+            "bytes_per_launch": per_launch, "blocks_per_launch": info["n_blocks"]}
+
+
+def _timed(rk, torch, fn):
+    """barrier + device sync on both sides of fn(); wall seconds, max over ranks (RCCL)."""
+    rk.barrier()
+    _sync(torch)
+    t0 = time.perf_counter()
+    res = fn()
+    _sync(torch)
+    rk.barrier()
+    el = time.perf_counter() - t0
+    return rk.max([el])[0], res
+
+
+def bench_frame(args, rk, torch):
+    """C2 (headline) / C3: one independent frame per rank, R rounds per step."""
     import picp_amd
     from picp_amd import synth
-
-    wl = dict(WORKLOADS[args.workload])
-    if args.workload == "c5":
-        return bench_vo(args, wl, world, rank, local, dist, torch)
+    wl = WORKLOADS[args.workload]
     n = args.n or wl["n"]
-    nprob = args.problems or wl["problems"]
     R = args.rounds
-    thr = 3000.0
-
-    # ---- inputs (seeded, resident on the device before timing) ----
-    if nprob == 1:
-        p = synth.make_problem(n, seed=42 + rank, outlier_frac=wl["outlier"], pixel_noise=0.5, shuffle=False)
-        xyz, uv, T_init, T_gt = p["xyz"], p["uv"], p["T_init"][None], p["T_gt"][None]
-        sizes = [n]
-    else:
-        bt = synth.make_batch(nprob, n, base_seed=1000, first=rank * nprob,
-                              outlier_frac=wl["outlier"], pixel_noise=0.5)
-        xyz, uv, T_init, T_gt, sizes = bt["xyz"], bt["uv"], bt["T_init"], bt["T_gt"], bt["sizes"]
-    b = picp_amd.Batch(sizes, device=local if world > 1 else 0)
+    p = synth.make_problem(n, seed=42 + rk.rank, outlier_frac=wl["outlier"], pixel_noise=0.5, shuffle=False)
+    xyz, uv, T_init, T_gt = p["xyz"], p["uv"], p["T_init"][None], p["T_gt"][None]
+    b = picp_amd.Batch([n], device=rk.device)
     b.set_data(xyz, uv)
     b.set_poses(T_init)
-    params = dict(threshold=thr, max_rounds=R, conv_eps=-1.0)
-
-    def sync_all():
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
+    params = dict(threshold=THRESHOLD, max_rounds=R, conv_eps=-1.0)
     for _ in range(args.warmup):
         b.solve_async(**params)
     b.sync()
-    sync_all()
+    # the K timed steps: K back-to-back fused solves on the library's stream, between HIP events
+    elapsed, (ev_ms, launch_us) = _timed(rk, torch, lambda: b.time(args.steps, **params))
+    err = rk.max([synth.se3_log_norm(b.poses()[0], T_gt[0])])[0]
 
-    barrier()
-    sync_all()
-    t0 = time.perf_counter()
-    # the K timed steps: K graph replays on the library's stream, bracketed by HIP events
-    ev_ms, (launch_us, pair_us) = b.time(args.steps, **params)
-    sync_all()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # ---- correctness of what was timed (outside the timed region) ----
-    poses = b.poses()
-    err = max(synth.se3_log_norm(poses[i], T_gt[i]) for i in range(len(sizes)))
-    if dist is not None:
-        from picp_amd.dist import gather_rows
-        # RCCL all-gather over xGMI: the only collective of the batch split (after timing)
-        allp = gather_rows(poses.reshape(len(sizes), 16), world * len(sizes), dist, device="cuda")
-        assert allp.shape == (world * len(sizes), 16)
-        errs = torch.tensor([err], dtype=torch.float64, device="cuda")
-        dist.all_reduce(errs, op=dist.ReduceOp.MAX)
-        err = float(errs.item())
-
-    # ---- roofline of the round kernel: algorithmic bytes per launch / mean launch duration,
-    #      the duration from the HIP events around the timed region (launches back to back) ----
     info = b.info()
-    # graph mode: one launch = one round over every correspondence; persistent/block mode: one
-    # launch = the whole R-round solve
-    corr_per_launch = int(info["total_corr"]) * (1 if info["mode"] == "graph" else R)
-    achieved = BYTES_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
-
-    # HBM traffic per launch from the committed PMC passes of the same default command
-    # (tools/gpu_pmc.sh): C2 / C3 persistent kernel, C4 block kernel
-    pmc_name = {("c2", "persistent"): "c2_persistent", ("c3", "persistent"): "c3_persistent",
-                ("c4", "block"): "c4_block"}.get((args.workload, info["mode"]))
-    default_cfg = (n == wl["n"] and len(sizes) == wl["problems"] and R == 50)
-    traffic, tsrc = pmc_traffic(pmc_name) if (pmc_name and default_cfg) else (None, None)
-    rounds_total = world * len(sizes) * R * args.steps
-    value = rounds_total / elapsed
+    default_cfg = (n == wl["n"] and R == 50)
+    pmc_name = {("c2", "persistent"): "c2_persistent", ("c3", "persistent"): "c3_persistent"}.get(
+        (args.workload, info["mode"])) if default_cfg else None
+    roof = _roofline(b, R, launch_us, pmc_name)
+    roof["timed_region_event_ms"] = round(ev_ms, 4)
+    if info["mode"] == "persistent":
+        roof["latency"] = _latency(launch_us, R)
+    value = rk.world * R * args.steps / elapsed
     out = {
         "metric": "PICP iterations/sec @ %d correspondences" % n,
         "value": round(value, 2),
         "unit": "iterations/s",
-        "n_gpus": world,
+        "n_gpus": rk.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
@@ -167,93 +284,160 @@ def main():
         "config": {
             "workload": wl["desc"],
             "n_corr": n,
-            "frames_per_gpu": len(sizes),
+            "frames_per_gpu": 1,
             "rounds": R,
-            "threshold": thr,
+            "threshold": THRESHOLD,
             "convergence_test": "disabled for timing",
-            "parallelism": "independent frames, one process per GPU" if world > 1 else "single GPU",
+            "parallelism": ("independent frames (seed 42 + rank), one process per GPU, RCCL world %d" % rk.world)
+                           if rk.world > 1 else "single GPU",
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic,
-            "traffic_source": tsrc,
-            "kernel": {"graph": "picp_round_kernel (one GN round per launch)",
-                       "persistent": "picp_persistent_kernel (all GN rounds in one launch)",
-                       "block": "picp_block_kernel (all GN rounds, one block per frame)"}[info["mode"]],
-            "mode": info["mode"],
-            "kernel_us": round(launch_us, 3),
-            "kernel_us_event_pair": round(pair_us, 3),
-            "timed_region_event_ms": round(ev_ms, 4),
-            "bytes_per_launch": BYTES_PER_CORR * corr_per_launch,
-            "blocks_per_launch": info["n_blocks"],
-        },
+        "roofline": roof,
         "pose_err_vs_gt_se3": err,
+        "residency": b.residency(),
     }
-    if args.workload in ("c2", "c3") and not args.skip_extras:
+    if rk.world > 1:
+        out["ranks"] = {"world_size_observed": rk.comm.world, "partition": "rank r solves frame seed 42 + r"}
+    if not args.skip_extras:
+        # diagnostic after the timed region: one solve with an event pair around its launch
+        out["roofline"]["kernel_us_event_pair"] = round(b.time_single(**params), 3)
+    if args.workload in ("c2", "c3") and not args.skip_extras and rk.world == 1:
         # C2 is timed with exactly R rounds; also report the icp_test loop with its
         # convergence test on (exec/icp_test.cpp:99-106), measured after the timed region
         cparams = dict(params, conv_eps=1e-5)
         b.solve(**cparams)
-        rounds_run = max(int(st["rounds"]) for st in b.stats())
+        rounds_run = int(b.stats()[0]["rounds"])
         cms, _ = b.time(args.steps, **cparams)
         per_solve_ms = cms / args.steps
         out["with_convergence"] = {
             "conv_eps": 1e-5, "rounds_run": rounds_run, "ms_per_solve": round(per_solve_ms, 4),
-            "iterations_per_s": round(len(sizes) * rounds_run / (per_solve_ms * 1e-3), 1),
-            "pose_err_vs_gt_se3": max(synth.se3_log_norm(b.poses()[i], T_gt[i]) for i in range(len(sizes))),
+            "iterations_per_s": round(rounds_run / (per_solve_ms * 1e-3), 1),
+            "pose_err_vs_gt_se3": synth.se3_log_norm(b.poses()[0], T_gt[0]),
         }
-    if args.workload == "c3" and not args.skip_extras:
-        # also with keep_outliers = true (outliers weighted by the robust
-        # lambda = sqrt(threshold / chi), src/picp_solver.cpp:80-88), measured after the timed region
-        kparams = dict(params, keep_outliers=1)
-        b.set_poses(T_init)
-        b.solve(**kparams)
-        kerr = max(synth.se3_log_norm(b.poses()[i], T_gt[i]) for i in range(len(sizes)))
-        kms, _ = b.time(args.steps, **kparams)
-        out["keep_outliers_true"] = {
-            "rounds": R, "ms_per_solve": round(kms / args.steps, 4),
-            "iterations_per_s": round(len(sizes) * R / (kms / args.steps * 1e-3), 1),
+    if args.workload == "c3" and not args.skip_extras and rk.world == 1:
+        out["keep_outliers_true"] = _keep_outliers_leg(b, T_init, T_gt, params, args.steps)
+    if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(xyz, uv, T_init[0], R, args.cpu_seconds)
+        if args.workload == "c2":
+            out["cpu_baseline_all_cores"] = cpu_baseline_mt(xyz, uv, T_init[0], R, max(2.0, args.cpu_seconds / 2))
+    del b
+    if args.workload == "c2" and not args.skip_extras:
+        if args.stream_n > 0 and rk.world == 1:
+            out["roofline_streaming"] = streaming_roofline(args.stream_n, R, rk.device)
+        # the other BASELINE configs, compact, on the same line (bounded time)
+        sub = argparse.Namespace(**vars(args))
+        sub.steps = max(5, min(args.steps, 10))
+        sub.warmup = 2
+        sub.cpu_seconds = 3.0
+        sub.n = sub.problems = sub.frames = sub.obs = 0
+        out["c4"] = _compact(bench_c4(sub, rk, torch))
+        if rk.world == 1:
+            sub.workload = "c3"
+            sub.skip_extras = True
+            out["c3"] = _compact(bench_frame(sub, rk, torch))
+        out["c5"] = _compact(bench_vo(sub, rk, torch))
+    return out
+
+
+def _compact(d):
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "roofline", "cpu_baseline",
+            "pose_err_vs_gt_se3", "pose_err_vs_gt_se3_max", "kernel_us", "kernel", "traffic", "traffic_source",
+            "picp_iterations_per_s", "ranks", "config")
+    out = {k: d[k] for k in keep if k in d}
+    if "config" in out:
+        out["config"] = {k: v for k, v in out["config"].items() if k in ("workload", "frames_total", "frames", "parallelism")}
+    return out
+
+
+def _latency(launch_us, R):
+    """C2's persistent kernel against its per-round latency floor: a round needs one reduction of
+    every block's partial to the leader and one broadcast of the new pose back (two dependent
+    cross-CU hand-offs, MI355X_MICROARCH.md handoff-1to1: 0.8 us each on an idle chip), plus the
+    compute on the critical path; the floor counts only the two hops."""
+    per_round = launch_us / max(R, 1)
+    floor = 2 * HANDOFF_US
+    return {"per_round_us": round(per_round, 3), "floor_us": floor, "frac": round(floor / per_round, 4),
+            "floor_basis": "2 x handoff-1to1 (fan-in of the block partials + fan-out of the pose), "
+                           "MI355X_MICROARCH.md price list; compute on the critical path excluded",
+            "phases": "DESIGN.md §4.3 (stamp logs under profiles/)"}
+
+
+def _keep_outliers_leg(b, T_init, T_gt, params, steps):
+    """also with keep_outliers = true (outliers weighted by the robust
+    lambda = sqrt(threshold / chi), src/picp_solver.cpp:80-88), measured after the timed region."""
+    from picp_amd import synth
+    kparams = dict(params, keep_outliers=1)
+    b.set_poses(T_init)
+    b.solve(**kparams)
+    kerr = synth.se3_log_norm(b.poses()[0], T_gt[0])
+    kms, _ = b.time(steps, **kparams)
+    return {"rounds": params["max_rounds"], "ms_per_solve": round(kms / steps, 4),
+            "iterations_per_s": round(params["max_rounds"] / (kms / steps * 1e-3), 1),
             "pose_err_vs_gt_se3": kerr,
             "note": "outliers are weighted by the robust lambda, not rejected: the pose is biased by them "
-                    "by design (the reference's keep_outliers mode); parity with the oracle is tested",
-        }
-    if args.workload == "c2" and args.stream_n > 0 and world == 1:
-        out["roofline_streaming"] = streaming_roofline(args.stream_n, R, thr, local if world > 1 else 0)
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(xyz[: sizes[0]], uv[: sizes[0]], T_init[0], R, thr, args.cpu_seconds)
-        out["cpu_baseline_all_cores"] = cpu_baseline_mt(xyz[: sizes[0]], uv[: sizes[0]], T_init[0], R, thr,
-                                                        max(2.0, args.cpu_seconds / 2))
-    if rank == 0:
-        print(json.dumps(out))
-    if dist is not None:
-        dist.destroy_process_group()
+                    "by design (the reference's keep_outliers mode); parity with the oracle is tested"}
 
 
-def pmc_traffic(name, fetch_scale=2.0):
-    """HBM bytes per launch from the newest committed rocprofv3 PMC passes of the same command
-    (profiles/rNN/<name>_pmc_{FETCH_SIZE,WRITE_SIZE}.json, written by tools/gpu_pmc*.sh from two
-    separate --pmc passes).  FETCH_SIZE x fetch_scale (gfx950: x2 for wide coalesced streams,
-    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB.  (None, None) when absent: bench.py
-    cannot collect PMC counters live."""
-    import glob
-    import json as _json
-    dirs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*")))
-    for d in reversed(dirs):
-        f, w = (os.path.join(d, "%s_pmc_%s.json" % (name, c)) for c in ("FETCH_SIZE", "WRITE_SIZE"))
-        if os.path.exists(f) and os.path.exists(w):
-            fk = _json.load(open(f))["FETCH_SIZE"]["mean"]
-            wk = _json.load(open(w))["WRITE_SIZE"]["mean"]
-            src = "%s (FETCH_SIZE %.1f KiB x %g + WRITE_SIZE %.1f KiB per launch)" % (
-                os.path.relpath(f, ROOT).replace("FETCH_SIZE", "{FETCH,WRITE}_SIZE"), fk, fetch_scale, wk)
-            return round((fk * fetch_scale + wk) * 1024.0), src
-    return None, None
+def bench_c4(args, rk, torch):
+    """C4: the fixed batch of 1024 frames x 10k split over the ranks (picp_shard_range); one step =
+    one fused 50-round solve of this rank's frames; the timed region ends with the RCCL all-gather
+    of every frame's pose + stats to every rank (C-ABI picp_batch_allgather)."""
+    import numpy as np
+    import picp_amd
+    from picp_amd import synth
+    wl = WORKLOADS["c4"]
+    n = args.n or wl["n"]
+    total = args.problems or wl["problems"]
+    R = args.rounds
+    f0, f1 = picp_amd.shard_range(total, rk.world, rk.rank)
+    bt = synth.make_batch(f1 - f0, n, base_seed=1000, first=f0, outlier_frac=0.0, pixel_noise=0.5)
+    b = picp_amd.Batch(bt["sizes"], device=rk.device)
+    b.set_data(bt["xyz"], bt["uv"])
+    b.set_poses(bt["T_init"])
+    params = dict(threshold=THRESHOLD, max_rounds=R, conv_eps=-1.0)
+    for _ in range(max(args.warmup, 1)):
+        b.solve_async(**params)
+    b.sync()
+
+    def job():
+        r = b.time(args.steps, **params)
+        if rk.comm is not None:
+            return r, rk.comm.allgather_batch(b, total)[0]
+        return r, b.poses()
+
+    elapsed, ((ev_ms, launch_us), allT) = _timed(rk, torch, job)
+    err = max(synth.se3_log_norm(b.poses()[i], bt["T_gt"][i]) for i in range(f1 - f0))
+    err = rk.max([err])[0]
+    mine = np.array_equal(allT[f0:f1], b.poses())  # the gather put this rank's rows in place
+    info = b.info()
+    # PMC passes of this exact command (1024 frames on one GPU): tools/gpu_pmc_r02.sh
+    pmc = "c4x1024_block" if (info["mode"] == "block" and n == wl["n"] and total == wl["problems"]
+                              and rk.world == 1 and R == 50) else None
+    roof = _roofline(b, R, launch_us, pmc)
+    out = {
+        "metric": "PICP iterations/sec, batch of %d frames x %d correspondences" % (total, n),
+        "value": round(total * R * args.steps / elapsed, 2),
+        "unit": "iterations/s",
+        "n_gpus": rk.world,
+        "steps": args.steps,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+        "scaling": "strong",
+        "roofline": roof,
+        "pose_err_vs_gt_se3": err,
+        "config": {"workload": wl["desc"], "frames_total": total, "frames_this_rank": f1 - f0,
+                   "parallelism": "picp_shard_range over %d ranks, one RCCL all-gather of results per job" % rk.world
+                   if rk.world > 1 else "single GPU"},
+    }
+    if rk.world > 1:
+        out["ranks"] = {"world_size_observed": rk.comm.world,
+                        "partition": [list(picp_amd.shard_range(total, rk.world, r)) for r in range(rk.world)],
+                        "allgather_rows_match_local": bool(rk.max([0.0 if mine else 1.0])[0] == 0.0)}
+    if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
+        sz = int(bt["sizes"][0])
+        out["cpu_baseline"] = cpu_baseline(bt["xyz"][:sz], bt["uv"][:sz], bt["T_init"][0], R, args.cpu_seconds)
+    return out
 
 
-def streaming_roofline(n, R, thr, device):
+def streaming_roofline(n, R, device):
     """The same solve on one frame large enough to stream from HBM every round (SURVEY.md §8d:
     a > 256 MB working set, past the 256 MB Infinity Cache): 20 B x n per round-launch of
     picp_round_kernel.  Reported beside the C2 line, whose single 100k frame is latency-bound."""
@@ -263,41 +447,40 @@ def streaming_roofline(n, R, thr, device):
     b = picp_amd.Batch([n], device=device)
     b.set_data(p["xyz"], p["uv"])
     b.set_poses(p["T_init"][None])
-    params = dict(threshold=thr, max_rounds=R, conv_eps=-1.0)
+    params = dict(threshold=THRESHOLD, max_rounds=R, conv_eps=-1.0)
     b.solve(**params)
-    ev_ms, (launch_us, _) = b.time(5, **params)
+    ev_ms, launch_us = b.time(5, **params)
     info = b.info()
-    launches = 1 if info["mode"] == "graph" else 0
-    per_launch = BYTES_PER_CORR * n * (1 if launches else R)
+    graph = info["mode"] == "graph"
+    per_launch = BYTES_PER_CORR * n * (1 if graph else R)
     achieved = per_launch / (launch_us * 1e-6) / 1e9
     err = synth.se3_log_norm(b.poses()[0], p["T_gt"])
-    traffic, tsrc = pmc_traffic("stream16m") if (n == 16000000 and launches) else (None, None)
+    traffic, tsrc = pmc_traffic("stream16m") if (n == 16000000 and graph) else (None, None)
     return {"bound": "hbm", "n_corr": n, "working_set_MB": round(BYTES_PER_CORR * n / 1e6, 1),
-            "kernel": "picp_round_kernel (one GN round per launch)" if launches else info["mode"],
-            "mode": info["mode"], "blocks_per_launch": info["n_blocks"], "kernel_us": round(launch_us, 3),
-            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "kernel": _kernel_name(info["mode"]), "mode": info["mode"], "blocks_per_launch": info["n_blocks"],
+            "kernel_us": round(launch_us, 3), "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
             "bytes_per_launch": per_launch, "iterations_per_s": round(R * 5 / (ev_ms * 1e-3), 2),
             "pose_err_vs_gt_se3": err}
 
 
-def bench_vo(args, wl, world, rank, local, dist, torch):
+def bench_vo(args, rk, torch):
     """C5: the whole sequence is split into contiguous segments of --seg-len PICP steps (one-frame
     overlap); ranks take contiguous ranges of segments (strong scaling: the
-    sequence is fixed).  One step = one replay of the captured run of this rank's segments
-    (pair matching of all its frames, bootstrap, then per frame: world match, gather, PICP block
-    kernel, triangulate/append).  value = frames estimated by all ranks / max-over-ranks time."""
+    sequence is fixed).  One step = one run of this rank's segments (pair matching of all its
+    frames, bootstrap, then per frame: world match, gather, PICP block kernel, triangulate/append).
+    value = frames estimated by all ranks / max-over-ranks time."""
     import numpy as np
     import picp_amd
     from picp_amd import synth
-    from picp_amd.dist import shard_range
     from picp_amd.vo_synth import VOSequence, segments
+    wl = WORKLOADS["c5"]
     F = args.frames or wl["frames"]
     obs = args.obs or wl["obs"]
     L = args.seg_len
     seq = VOSequence(F, obs_per_frame=obs, seed=42)
     first, steps = segments(F, L)
-    s0, s1 = shard_range(len(first), world, rank)
+    s0, s1 = picp_amd.shard_range(len(first), rk.world, rk.rank)
     fa, fb = int(first[s0]), int(first[s1 - 1] + steps[s1 - 1])
     D = seq.frames(fa, fb + 1)
     my_first, my_steps = first[s0:s1] - fa, steps[s0:s1]
@@ -305,29 +488,11 @@ def bench_vo(args, wl, world, rank, local, dist, torch):
     # (exec/icp_test.cpp:36, bootstrap from Identity): float32 coordinates stay segment-sized
     rel = [np.linalg.inv(D["T_cw"][f].astype(np.float64)) for f in my_first]
     boot = np.stack([[np.eye(4), rel[k] @ D["T_cw"][f + 1]] for k, f in enumerate(my_first)]).astype(np.float32)
-    vo = picp_amd.VOSequence(D["frame_off"], D["uv"], D["desc"], device=local if world > 1 else 0, K=seq.K)
-    vo.set_segments(my_first, my_steps, boot, threshold=3000.0)
-
-    def sync_all():
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-
+    vo = picp_amd.VOSequence(D["frame_off"], D["uv"], D["desc"], device=rk.device, K=seq.K)
+    vo.set_segments(my_first, my_steps, boot, threshold=THRESHOLD)
     for _ in range(max(args.warmup, 1)):
         vo.run()
-    sync_all()
-    if dist is not None:
-        dist.barrier()
-    sync_all()
-    t0 = time.perf_counter()
-    ev_ms = vo.time(args.steps)
-    sync_all()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, ev_ms = _timed(rk, torch, lambda: vo.time(args.steps))
     # correctness of what was timed: drift vs gt, PICP work done
     P, Rr = vo.poses(), vo.step_records()
     err, rounds, corr = 0.0, 0, 0
@@ -337,21 +502,15 @@ def bench_vo(args, wl, world, rank, local, dist, torch):
             err = max(err, synth.se3_log_norm(P[k][t].astype(np.float64), gt))
         rounds += int(Rr[k]["rounds"][1:].sum())
         corr += int((Rr[k]["rounds"][1:].astype(np.int64) * Rr[k]["n_corr"][1:]).sum())
-    stats = np.array([err, rounds, corr, int(my_steps.sum())], np.float64)
-    if dist is not None:
-        t = torch.tensor(stats, device="cuda")
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        e = t[:1].clone()
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        stats = t.cpu().numpy()
-        stats[0] = float(e.item())
-    frames_total = int(stats[3])
+    err = rk.max([err])[0]
+    tot = rk.gather_obj([rounds, corr, int(my_steps.sum())])
+    rounds, corr, frames_total = (sum(t[i] for t in tot) for i in range(3))
     info = vo.info()
     out = {
         "metric": "VO frames/sec (%d-frame synthetic sequence, ~%d obs/frame, per-frame match + PICP + triangulate)" % (F, obs),
         "value": round(frames_total * args.steps / elapsed, 2),
         "unit": "frames/s",
-        "n_gpus": world,
+        "n_gpus": rk.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
@@ -361,23 +520,47 @@ def bench_vo(args, wl, world, rank, local, dist, torch):
         "dtype": "f32",
         "data": "synthetic sequence (picp_amd/vo_synth.py, seed 42; observations resident in HBM)",
         "config": {"workload": wl["desc"], "frames": F, "obs_per_frame": obs, "segment_steps": L,
-                   "segments": len(first), "segments_per_gpu": s1 - s0, "threshold": 3000.0,
+                   "segments": len(first), "segments_this_rank": s1 - s0, "threshold": THRESHOLD,
                    "picp_loop": "icp_test: <= 50 rounds, relative chi convergence 1e-5",
-                   "parallelism": "contiguous segment ranges, one process per GPU" if world > 1 else "single GPU",
+                   "parallelism": "contiguous segment ranges (picp_shard_range), one process per GPU"
+                   if rk.world > 1 else "single GPU",
                    "block_npt": info["npt"]},
-        "picp_iterations_per_s": round(stats[1] * args.steps / elapsed, 1),
-        "picp_corr_rounds_per_s": round(stats[2] * args.steps / elapsed, 1),
+        "picp_iterations_per_s": round(rounds * args.steps / elapsed, 1),
+        "picp_corr_rounds_per_s": round(corr * args.steps / elapsed, 1),
         "timed_region_event_ms": round(ev_ms * args.steps, 4),
-        "pose_err_vs_gt_se3_max": stats[0],
+        "pose_err_vs_gt_se3_max": err,
         "pose_err_frame": "camera-in-world poses in each segment's frame (its first camera)",
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rk.world > 1:
+        out["ranks"] = {"world_size_observed": rk.comm.world,
+                        "partition": [list(picp_amd.shard_range(len(first), rk.world, r)) for r in range(rk.world)]}
+    if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
-        out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
-    if rank == 0:
-        print(json.dumps(out))
-    if dist is not None:
-        dist.destroy_process_group()
+        if args.workload == "c5":
+            out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
+    return out
+
+
+def plan_only(args, rk):
+    """--plan-only (no GPU, gloo): every rank shards the workloads exactly as a GPU run would,
+    builds its C4 inputs, and rank 0 gathers (rank, shard, input checksum) -- the CPU test of the
+    multi-process launcher."""
+    import numpy as np
+    from picp_amd import synth
+    from picp_amd.dist import shard_range
+    total = args.problems or WORKLOADS["c4"]["problems"]
+    n = args.n or 256
+    f0, f1 = shard_range(total, rk.world, rk.rank)
+    bt = synth.make_batch(f1 - f0, n, base_seed=1000, first=f0)
+    from picp_amd.vo_synth import segments
+    first, _ = segments(args.frames or WORKLOADS["c5"]["frames"], args.seg_len)
+    mine = {"rank": rk.rank, "pid": os.getpid(), "local_rank": rk.local, "c2_seed": 42 + rk.rank,
+            "c4_frames": [f0, f1], "c4_checksum": float(np.float64(bt["xyz"]).sum() + np.float64(bt["uv"]).sum()),
+            "c5_segments": list(shard_range(len(first), rk.world, rk.rank))}
+    allm = rk.gather_obj(mine)
+    if rk.rank == 0:
+        print(json.dumps({"plan_only": True, "n_gpus": args.gpus, "world_size_observed": rk.world,
+                          "backend": "gloo" if rk.dist is not None else "none", "ranks": allm}), flush=True)
 
 
 def cpu_baseline_vo(seq, L, budget_s):
@@ -449,7 +632,7 @@ def _cpu_model():
     return model
 
 
-def cpu_baseline_mt(xyz, uv, T_init, R, thr, budget_s):
+def cpu_baseline_mt(xyz, uv, T_init, R, budget_s):
     """SURVEY.md §8d's all-cores CPU baseline for C2/C3: the oracle's loop with the linearize as a
     chunked reduction over OMP_NUM_THREADS threads (the box's CPU share; os.cpu_count() shows the
     whole machine).  Timing only; its pose is checked against the sequential oracle's."""
@@ -461,8 +644,8 @@ def cpu_baseline_mt(xyz, uv, T_init, R, thr, budget_s):
     Kref = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
     solves, t0 = 0, time.perf_counter()
     while True:
-        T_mt, _ = O.solve_soa_mt(T_init, Kref, 480, 640, x, y, z, u, v, thr, threads,
-                                 mode=O.MODE_FAITHFUL, max_rounds=R, conv_eps=-1.0)
+        O.solve_soa_mt(T_init, Kref, 480, 640, x, y, z, u, v, THRESHOLD, threads,
+                       mode=O.MODE_FAITHFUL, max_rounds=R, conv_eps=-1.0)
         solves += 1
         el = time.perf_counter() - t0
         if el >= budget_s:
@@ -473,18 +656,17 @@ def cpu_baseline_mt(xyz, uv, T_init, R, thr, budget_s):
                       "-march=x86-64-v3) in %.1f s on %s" % (solves, R, len(x), threads, el, _cpu_model())}
 
 
-def cpu_baseline(xyz, uv, T_init, R, thr, budget_s):
+def cpu_baseline(xyz, uv, T_init, R, budget_s):
     """Oracle (faithful float32, sequential) single thread on one frame of the workload:
     whole R-round solves until the time budget is used (at least one)."""
     import numpy as np
     import oracle as O
     x, y, z = (np.ascontiguousarray(xyz[:, i]) for i in range(3))
     u, v = np.ascontiguousarray(uv[:, 0]), np.ascontiguousarray(uv[:, 1])
-    K = O._k9  # noqa: F841  (ensure module import)
     Kref = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
     solves, t0 = 0, time.perf_counter()
     while True:
-        O.solve_soa(T_init, Kref, 480, 640, x, y, z, u, v, thr, mode=O.MODE_FAITHFUL,
+        O.solve_soa(T_init, Kref, 480, 640, x, y, z, u, v, THRESHOLD, mode=O.MODE_FAITHFUL,
                     max_rounds=R, conv_eps=-1.0)
         solves += 1
         el = time.perf_counter() - t0

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PICP_ABI_VERSION 1
+#define PICP_ABI_VERSION 2
 
 /* status codes */
 #define PICP_OK 0
@@ -140,18 +140,57 @@ int picp_batch_solve(picp_batch_t* b, const picp_params* params);
 int picp_batch_solve_async(picp_batch_t* b, const picp_params* params);
 int picp_batch_sync(picp_batch_t* b);
 
-/* Run `reps` back-to-back fused solves (graph replays) on the batch's stream between two HIP
- * events.  total_ms = event time of the whole region; kernel_us[0] = mean launch period of the
- * round kernel in that region (total / (reps * (max_rounds + 1)) launches); kernel_us[1] =
- * mean of event pairs around single round launches (separate pass; includes event overhead).
- * Blocking; results readable with picp_batch_get_poses/stats afterwards. */
+/* Run `reps` back-to-back fused solves on the batch's stream between two HIP events and nothing
+ * else.  total_ms = event time of the whole region; launch_us (nullable) = mean launch period
+ * of the dominant kernel in it (total / (reps x launches per solve): max_rounds round launches in
+ * graph mode, one launch otherwise).  Blocking; results readable with picp_batch_get_poses/stats
+ * afterwards. */
 int picp_batch_time(picp_batch_t* b, const picp_params* params, int reps, float* total_ms,
-                    float kernel_us[2]);
+                    float* launch_us);
+/* Diagnostic: one solve with an event pair around every launch (graph mode: the mean over its
+ * round launches; otherwise the single launch), an upper bound that adds the event overhead. */
+int picp_batch_time_single(picp_batch_t* b, const picp_params* params, float* us);
 /* Introspection: total correspondences, blocks per launch, and the execution mode chosen for
  * the batch: 0 = one launch per GN round replayed from a hipGraph (any batch); 1 = the whole
- * loop in one persistent launch (batches whose blocks all fit on the device at once; env
- * PICP_MODE=graph forces 0). */
+ * loop in one persistent launch; 2 = one block (or a few cooperating blocks) per problem
+ * (env PICP_MODE=graph|persistent|block forces one where the batch is eligible). */
 int picp_batch_info(picp_batch_t* b, int64_t* total_corr, int* n_blocks, int* mode);
+/* Co-residency of the layout's cross-block hand-off launch (persistent mode, or block mode with
+ * two or four blocks per problem): grid = its blocks, resident = blocks the device holds at once
+ * for that kernel (occupancy query x CUs; 0/0 when the layout considered none).  Such a launch is
+ * used only when grid <= resident; if a hand-off wait still times out (CUs held by other work),
+ * the solve is re-run without hand-offs and the batch keeps that layout: fallbacks counts it. */
+int picp_batch_residency(picp_batch_t* b, int* grid, int* resident, int* fallbacks);
+
+/* ---------------- batch split across GPUs: one process per GPU ---------------- */
+
+/* The node's GPUs each run one process with its own picp_batch holding a contiguous shard of the
+ * independent problems; the only collective is one RCCL all-gather (over xGMI) of the results.
+ * The communicator wraps an RCCL communicator created from a 128-byte unique id that rank 0 makes
+ * with picp_comm_unique_id and the launcher hands to every rank out of band.  librccl is loaded
+ * on the first picp_comm_* call (dlopen), so single-GPU use never needs it. */
+#define PICP_COMM_ID_BYTES 128
+typedef struct picp_comm picp_comm_t;
+
+/* Contiguous balanced split of n_items over world ranks: rank owns [*first, *last); sizes differ
+ * by at most one (lower ranks take the remainder). */
+int picp_shard_range(int64_t n_items, int world, int rank, int64_t* first, int64_t* last);
+int picp_comm_unique_id(uint8_t id[PICP_COMM_ID_BYTES]);
+/* Collective over the world: blocks until every rank has joined. */
+int picp_comm_create(picp_comm_t** out, int device, int world, int rank,
+                     const uint8_t id[PICP_COMM_ID_BYTES]);
+int picp_comm_destroy(picp_comm_t* c);
+int picp_comm_info(picp_comm_t* c, int* device, int* world, int* rank);
+/* Element-wise max over ranks of n (1..64) host doubles, in place (e.g. the timed region's wall
+ * time); blocking. */
+int picp_comm_allreduce_max(picp_comm_t* c, double* values, int n);
+int picp_comm_barrier(picp_comm_t* c);
+/* After a solve of this rank's batch (which must hold exactly picp_shard_range(n_total, world,
+ * rank)'s problems): completes it, then all-gathers every rank's per-problem results so that
+ * T_all[16 * n_total] (column-major camera poses, problem order) and st_all[n_total] (nullable)
+ * hold all of them on every rank.  Collective: every rank calls it. */
+int picp_batch_allgather(picp_batch_t* b, picp_comm_t* c, int64_t n_total, float* T_all,
+                         picp_stats* st_all);
 
 /* ---------------- linear triangulation (cv::triangulatePoints replacement) ---------------- */
 

@@ -77,3 +77,32 @@ def test_gloo_world2_split_and_gather_matches_single_process():
         assert p.exitcode == 0
     ref = _solve_frames(0, n_frames, n_corr)
     np.testing.assert_array_equal(got, ref)
+
+
+def test_bench_launcher_gpus2_plan_only_starts_shards_and_gathers():
+    """`bench.py --gpus 2` (no WORLD_SIZE: the launcher starts the ranks itself, as the driver
+    invokes it) in --plan-only mode (gloo, no device): two distinct rank processes start, shard
+    C2 / C4 / C5 exactly as a GPU run would, and rank 0 gathers every rank's partition and the
+    checksum of the C4 inputs it built."""
+    import json
+    import subprocess
+    import sys
+    from picp_amd import synth
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plan-only",
+                        "--problems", "9", "--n", "64", "--frames", "200"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["plan_only"] and out["n_gpus"] == 2 and out["world_size_observed"] == 2
+    ranks = out["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1] and ranks[0]["pid"] != ranks[1]["pid"]
+    assert [x["c4_frames"] for x in ranks] == [[0, 5], [5, 9]]
+    assert [x["c2_seed"] for x in ranks] == [42, 43]
+    # 200 frames in 40-step segments -> 5 segments: 3 + 2
+    assert [x["c5_segments"] for x in ranks] == [[0, 3], [3, 5]]
+    for x in ranks:
+        f0, f1 = x["c4_frames"]
+        bt = synth.make_batch(f1 - f0, 64, base_seed=1000, first=f0)
+        assert x["c4_checksum"] == float(np.float64(bt["xyz"]).sum() + np.float64(bt["uv"]).sum())

@@ -1,0 +1,126 @@
+"""The batch split's C++ side on one GPU, and the co-residency guarantees of the hand-off kernels.
+
+* picp_comm_* (RCCL driven by libpicp_amd.so): a world-1 communicator's barrier, max-reduction
+  and the batch all-gather, whose rows must equal the batch's own results bit for bit.  (A world
+  > 1 RCCL communicator needs one GPU per rank; the N-rank path is covered on CPU by
+  tests/test_dist.py and runs on a node at round end.)
+* Residency: persistent and split-block launches are used only when the occupancy query says the
+  whole grid is resident; PICP_RESIDENT_BLOCKS_PER_CU=0 emulates a device held by other work and
+  must select the layouts without cross-block waits -- with the oracle's pose.
+* Fallback: a hand-off wait that times out (PICP_TIMEOUT_MS tiny: every wait expires) re-runs
+  the solve without hand-offs in the same call, returns the oracle's pose and counts it.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THR = 3000.0
+POSE_TOL = 1e-4
+
+
+def _problem_batch(native, sizes, seed0):
+    from picp_amd import synth
+    probs = [synth.make_problem(n, seed=seed0 + i, outlier_frac=0.1, pixel_noise=0.5, shuffle=False)
+             for i, n in enumerate(sizes)]
+    b = native.Batch(sizes)
+    b.set_data(np.concatenate([p["xyz"] for p in probs]), np.concatenate([p["uv"] for p in probs]))
+    b.set_poses(np.stack([p["T_init"] for p in probs]))
+    return b, probs
+
+
+def _oracle_pose(oracle, p, rounds=50, conv=-1.0):
+    T, st = oracle.solve_soa(p["T_init"], p["K"], 480, 640, p["x"], p["y"], p["z"], p["u"], p["v"], THR,
+                             mode=oracle.MODE_F64, max_rounds=rounds, conv_eps=conv)
+    return T, st
+
+
+def test_comm_world1_allgather_barrier_max(native):
+    uid = native.comm_unique_id()
+    assert len(uid) == native.COMM_ID_BYTES
+    c = native.Comm(0, 1, 0, uid)
+    try:
+        c.barrier()
+        np.testing.assert_array_equal(c.allreduce_max([1.5, -2.0, 3.25]), [1.5, -2.0, 3.25])
+        b, _ = _problem_batch(native, [3000, 17, 5000], 700)
+        b.solve(threshold=THR, max_rounds=20, conv_eps=-1.0)
+        T, st = c.allgather_batch(b, 3)
+        np.testing.assert_array_equal(T, b.poses())
+        assert [s["n_in"] for s in st] == [s["n_in"] for s in b.stats()]
+        # the batch must hold this rank's shard of n_total exactly
+        with pytest.raises(native.PicpError):
+            c.allgather_batch(b, 4)
+    finally:
+        c.close()
+
+
+def test_shard_range_c_abi_matches_python():
+    import picp_amd
+    from picp_amd.dist import shard_range
+    for n in (0, 1, 7, 1024, 1025):
+        for w in (1, 2, 3, 8):
+            for r in range(w):
+                assert picp_amd.shard_range(n, w, r) == shard_range(n, w, r)
+
+
+def test_persistent_residency_reported(native):
+    b, _ = _problem_batch(native, [100000], 42)
+    info, res = b.info(), b.residency()
+    assert info["mode"] == "persistent"
+    assert 0 < res["handoff_grid"] <= res["resident_blocks"] and res["fallbacks"] == 0
+
+
+@pytest.mark.parametrize("sizes,mode_hand,mode_safe", [([100000], "persistent", "graph"),
+                                                       ([10000] * 128, "block", "block")])
+def test_refused_residency_selects_layout_without_handoffs(native, oracle, sizes, mode_hand, mode_safe):
+    """PICP_RESIDENT_BLOCKS_PER_CU=0: the occupancy check refuses every hand-off grid, so a single
+    frame runs in graph mode and a 128-frame batch with one block per problem (no partner
+    exchange); the poses still match the oracle."""
+    os.environ["PICP_RESIDENT_BLOCKS_PER_CU"] = "0"
+    try:
+        b, probs = _problem_batch(native, sizes, 900)
+    finally:
+        os.environ.pop("PICP_RESIDENT_BLOCKS_PER_CU")
+    assert b.info()["mode"] == mode_safe
+    res = b.residency()
+    assert res["resident_blocks"] == 0 and res["handoff_grid"] > 0
+    b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
+    from picp_amd import synth
+    P = b.poses()
+    for i in range(0, len(sizes), max(1, len(sizes) // 8)):
+        T_ref, _ = _oracle_pose(oracle, probs[i])
+        assert synth.se3_log_norm(P[i], T_ref) < POSE_TOL, i
+    # and the same batch laid out normally agrees
+    b2, _ = _problem_batch(native, sizes, 900)
+    assert b2.info()["mode"] == mode_hand
+    b2.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
+    for i in range(len(sizes)):
+        assert synth.se3_log_norm(P[i], b2.poses()[i]) < POSE_TOL, i
+
+
+@pytest.mark.parametrize("sizes", [[100000], [10000] * 128])
+def test_timed_out_handoff_reruns_without_handoffs(native, oracle, sizes):
+    """Every hand-off wait expires (PICP_TIMEOUT_MS = 1e-4 ms): the persistent / split-block launch
+    ends with the error word set, the library lays the batch out without hand-offs, re-runs the
+    same solve from the same initial poses and returns the oracle's pose; fallbacks counts it and
+    later solves keep the safe layout."""
+    from picp_amd import synth
+    os.environ["PICP_TIMEOUT_MS"] = "0.0001"
+    try:
+        b, probs = _problem_batch(native, sizes, 1100)
+    finally:
+        os.environ.pop("PICP_TIMEOUT_MS")
+    before = b.info()["mode"]
+    b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
+    res = b.residency()
+    assert res["fallbacks"] == 1, (before, res)
+    assert b.info()["mode"] == ("graph" if before == "persistent" else "block")
+    P = b.poses()
+    for i in range(0, len(sizes), max(1, len(sizes) // 8)):
+        T_ref, _ = _oracle_pose(oracle, probs[i])
+        assert synth.se3_log_norm(P[i], T_ref) < POSE_TOL, i
+    b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
+    assert b.residency()["fallbacks"] == 1
+    np.testing.assert_array_equal(b.poses(), P)

@@ -130,3 +130,29 @@ def test_match_adversarial_fallbacks(native, oracle):
     # tiny magnitudes (fp16 subnormals)
     tiny = (rng.uniform(-1, 1, (400, 10)) * 1e-5).astype(np.float32)
     _eq(native.match_points(tiny[:150], tiny[150:], 1.0, 0.8), oracle.match_points(tiny[:150], tiny[150:], 1.0, 0.8))
+
+
+def test_match_batch_two_row_blocks(native, oracle, monkeypatch):
+    """The matcher's two-row-block form (RB = 2, 64 queries per wave), what the C5 sequence runs:
+    the accept-only form picks it by itself once n_problems x ceil(nq / 256) >= 4 x CUs (1024
+    problems of 200 queries here); PICP_MATCH_RB=2 forces it on the other forms.  Exact ties and
+    duplicated references (best = second, ratio 0/0 rejected) in every problem, problems of 1 and
+    0 queries and an empty reference set mixed in."""
+    if _MODE["kernel"] != "accept_only":
+        monkeypatch.setenv("PICP_MATCH_RB", "2")
+    rng = np.random.default_rng(2024)
+    d1s, d2s = [], []
+    for i in range(1024):
+        n1, n2 = (200, 300) if i % 97 else (1 if i % 2 else 0, 0 if i % 194 else 40)
+        d1, d2 = _sets(rng, n1, n2, 10, frac_true=0.7)
+        if n2 > 8:
+            d2[4] = d2[5]          # exact duplicate reference
+            d2[7] = d2[6] + 0.0
+            if n1 > 3:
+                d1[2] = d2[4]      # a query sitting on the duplicate: distance 0 twice
+                d1[3] = d2[6] + np.float32(1e-3)
+        d1s.append(d1)
+        d2s.append(d2)
+    outs = native.match_points_batch(d1s, d2s)
+    for d1, d2, got in zip(d1s, d2s, outs):
+        _eq(got, oracle.match_points(d1, d2))

@@ -46,9 +46,9 @@ def main():
     kus = {}
     for _ in range(args.interleave):
         for ipb, b in batches.items():
-            ms, (lin, fin) = b.time(args.reps, threshold=3000.0, max_rounds=args.rounds, conv_eps=-1.0)
+            ms, lin = b.time(args.reps, threshold=3000.0, max_rounds=args.rounds, conv_eps=-1.0)
             res[ipb].append(ms / args.reps)
-            kus[ipb] = (lin, fin)
+            kus[ipb] = (lin, b.time_single(threshold=3000.0, max_rounds=args.rounds, conv_eps=-1.0))
     corr = sum(sizes)
     for ipb, v in res.items():
         ms = float(np.median(v))
