@@ -48,6 +48,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_CORR = 20    # x,y,z,u,v float32 per correspondence-round
 HANDOFF_US = 0.8       # MI355X_MICROARCH.md price list, handoff-1to1 (idle, 8-B granule)
+FLOPS_PER_CORR = 160   # FP32 flops per correspondence-round (projection, J, J^T J, J^T e)
+VALU_PEAK_TFS = 157.3  # MI355X_MICROARCH.md chip table: peak FP32 vector
 
 WORKLOADS = {
     "c2": dict(n=100000, problems=1, outlier=0.0, desc="C2 single-frame PICP, 100k synthetic correspondences, 50 GN rounds"),
@@ -221,10 +223,26 @@ def _roofline(b, R, launch_us, pmc_name):
     per_launch = BYTES_PER_CORR * corr_per_launch
     achieved = per_launch / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
     traffic, tsrc = pmc_traffic(pmc_name) if pmc_name else (None, None)
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
-            "kernel": _kernel_name(info["mode"]), "mode": info["mode"], "kernel_us": round(launch_us, 3),
-            "bytes_per_launch": per_launch, "blocks_per_launch": info["n_blocks"]}
+    out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
+           "kernel": _kernel_name(info["mode"]), "mode": info["mode"], "kernel_us": round(launch_us, 3),
+           "bytes_per_launch": per_launch, "blocks_per_launch": info["n_blocks"]}
+    # the FP32 vector view: 160 flops per correspondence-round over the same launch period
+    tfs = FLOPS_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e12 if launch_us > 0 else 0.0
+    out["valu"] = {"achieved": round(tfs, 3), "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                   "frac": round(tfs / VALU_PEAK_TFS, 5), "flops_per_launch": FLOPS_PER_CORR * corr_per_launch}
+    return out
+
+
+def _resident_bound(roof):
+    """Sub-results whose frames stay in registers/LDS across rounds (counter traffic far below the
+    algorithmic bytes) are bound by VALU issue, not HBM: report the FP32 vector roofline as the
+    bound, the algorithmic-bytes rate beside it."""
+    if roof.get("traffic") is not None and roof["traffic"] < 0.25 * roof["bytes_per_launch"]:
+        v = roof.pop("valu")
+        roof["algorithmic_bytes_rate"] = {k: roof.pop(k) for k in ("achieved", "peak", "unit", "frac")}
+        roof.update({"bound": "valu", **v})
+    return roof
 
 
 def _timed(rk, torch, fn):
@@ -333,7 +351,9 @@ def bench_frame(args, rk, torch):
         if rk.world == 1:
             sub.workload = "c3"
             sub.skip_extras = True
-            out["c3"] = _compact(bench_frame(sub, rk, torch))
+            c3 = bench_frame(sub, rk, torch)
+            c3["roofline"] = _resident_bound(c3["roofline"])
+            out["c3"] = _compact(c3)
         out["c5"] = _compact(bench_vo(sub, rk, torch))
     return out
 
@@ -412,7 +432,7 @@ def bench_c4(args, rk, torch):
     # PMC passes of this exact command (1024 frames on one GPU): tools/gpu_pmc_r02.sh
     pmc = "c4x1024_block" if (info["mode"] == "block" and n == wl["n"] and total == wl["problems"]
                               and rk.world == 1 and R == 50) else None
-    roof = _roofline(b, R, launch_us, pmc)
+    roof = _resident_bound(_roofline(b, R, launch_us, pmc))
     out = {
         "metric": "PICP iterations/sec, batch of %d frames x %d correspondences" % (total, n),
         "value": round(total * R * args.steps / elapsed, 2),
