@@ -168,13 +168,8 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
     Acc2 a;
     acc2_zero(a);
-#pragma unroll
-    for (int k = 0; k < NPT; k += 2) {  // pairs (k, k+1); NPT == 1: slot B repeats item 0, masked
-      const int k1 = (k + 1 < NPT) ? k + 1 : k;
-      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]},
-                      (f2){zs[k], zs[k1]}, (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]},
-                      tid + k * BS < n, k + 1 < NPT && tid + (k + 1) * BS < n, a);
-    }
+    Cnt nr = {0u, 0u}, nd = {0u, 0u};  // counts: register items (uniform), divergent loops (lane 0)
+    accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
     for (int i = tid; i < n_lds; i += 2 * BS) {  // LDS-staged items, in pairs
       const int i2 = min(i + BS, n_lds - 1);
       // scalar locals first: building the f2 operands from the LDS reads directly made the
@@ -182,19 +177,19 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
       const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
       accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
-                      (f2){v0, v1}, true, i + BS < n_lds, a);
+                      (f2){v0, v1}, true, i + BS < n_lds, a, nd);
     }
     for (int i = r0 + n_lds + tid; i < n; i += 2 * BS) {  // streamed remainder
       const int i2 = min(i + BS, n - 1);
       const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
       const float x1 = X[base + i2], y1 = Y[base + i2], z1 = Z[base + i2], u1 = U[base + i2], v1 = V[base + i2];
       accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
-                      (f2){v0, v1}, true, i + BS < n, a);
+                      (f2){v0, v1}, true, i + BS < n, a, nd);
     }
     float v[PICP_NPART];
     BSTAMP(1);
     acc2_fold(a, v);
-    const float wsum = wave_reduce32(v, lane);
+    const float wsum = wave_counts(wave_reduce32(v, lane), lane, (Cnt){nr.n_in + nd.n_in, nr.n_proj + nd.n_proj});
     if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
     BSTAMP(2);
     __syncthreads();
@@ -293,37 +288,54 @@ static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out)
   return (size_t)5 * lds_items * sizeof(float);
 }
 
-template <int N>
-static const void* block_kernel_n(bool ph, int bs) {
-  if (bs == 256) return ph ? (const void*)picp_block_kernel<N, 1, 256> : (const void*)picp_block_kernel<N, 0, 256>;
-  return ph ? (const void*)picp_block_kernel<N, 1, 512> : (const void*)picp_block_kernel<N, 0, 512>;
+template <int N, int B>
+static const void* block_kernel_nb(int var) {
+  switch (var) {
+    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, B>;
+    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, B>;
+    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, B>;
+  }
 }
 
-static const void* block_kernel_ptr(int npt, bool ph, int bs) {
+template <int N>
+static const void* block_kernel_n(int var, int bs) {
+  return (bs == 256) ? block_kernel_nb<N, 256>(var) : block_kernel_nb<N, 512>(var);
+}
+
+static const void* block_kernel_ptr(int npt, int var, int bs) {
   switch (npt) {
-    case 1: return block_kernel_n<1>(ph, bs);
-    case 2: return block_kernel_n<2>(ph, bs);
-    case 4: return block_kernel_n<4>(ph, bs);
-    case 8: return block_kernel_n<8>(ph, bs);
+    case 1: return block_kernel_n<1>(var, bs);
+    case 2: return block_kernel_n<2>(var, bs);
+    case 4: return block_kernel_n<4>(var, bs);
+    case 8: return block_kernel_n<8>(var, bs);
     default: return nullptr;
   }
 }
 
-// Blocks of the variant a launch with these arguments uses that one CU holds at once (the
-// hardware limit from registers, LDS and waves; other work on the device is not counted).  The
-// host multiplies by the CU count and launches a split grid (whose blocks wait on each other)
-// only if the whole grid fits.
+// Blocks of the variants a launch with these arguments may use that one CU holds at once (the
+// hardware limit from registers, LDS and waves; other work on the device is not counted; the
+// smaller of the two pinhole variants, since keep_outliers is a per-solve argument).  The host
+// multiplies by the CU count and launches a split grid (whose blocks wait on each other) only if
+// the whole grid fits.
 extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu) {
   if (!blocks_per_cu || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
   const int bs = (split == 4) ? 256 : PICP_BBLOCK;
-  const void* fn = block_kernel_ptr(npt, picp_use_pinhole(K), bs);
-  if (!fn) return hipErrorInvalidValue;
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr);
-  if (lds_bytes > 65536) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  int best = -1;
+  for (int keep = 0; keep < 2; ++keep) {
+    const void* fn = block_kernel_ptr(npt, picp_variant(K, keep), bs);
+    if (!fn) return hipErrorInvalidValue;
+    if (lds_bytes > 65536) {
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+      if (e != hipSuccess) return e;
+    }
+    int occ = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, bs, lds_bytes);
     if (e != hipSuccess) return e;
+    best = (best < 0 || occ < best) ? occ : best;
   }
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, bs, lds_bytes);
+  *blocks_per_cu = best;
+  return hipSuccess;
 }
 
 // max_n: the largest problem of the launch (sizes the LDS stage: max_n/split - npt*BS items,
@@ -341,7 +353,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
   if (n_problems <= 0 || !args || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
   if (split > 1 && (!xg || !err || !tagbase)) return hipErrorInvalidValue;
   const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
-  const bool ph = picp_use_pinhole(args->K);
+  const int var = picp_variant(args->K, args->keep_outliers);
   const int bs = (split == 4) ? 256 : PICP_BBLOCK;
   int lds_items = 0;
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, &lds_items);
@@ -353,11 +365,15 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
     hipLaunchKernelGGL((picp_block_kernel<N, P, B>), dim3(grid), dim3(B), lds_bytes, stream, X, Y, Z, U, V, \
                        *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, tagbase, timeout_ticks); \
   }
-#define PICP_LAUNCH_B(N)                              \
-  if (bs == 256) {                                    \
-    if (ph) PICP_LAUNCH_B3(N, 1, 256) else PICP_LAUNCH_B3(N, 0, 256) \
-  } else {                                            \
-    if (ph) PICP_LAUNCH_B3(N, 1, 512) else PICP_LAUNCH_B3(N, 0, 512) \
+#define PICP_LAUNCH_BV(N, B)                                                              \
+  if (var == PICP_V_PINHOLE) PICP_LAUNCH_B3(N, PICP_V_PINHOLE, B)                           \
+  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_B3(N, PICP_V_PINHOLE_KEEP, B)            \
+  else PICP_LAUNCH_B3(N, PICP_V_GENERAL, B)
+#define PICP_LAUNCH_B(N)   \
+  if (bs == 256) {         \
+    PICP_LAUNCH_BV(N, 256) \
+  } else {                 \
+    PICP_LAUNCH_BV(N, 512) \
   }
   switch (npt) {
     case 1: PICP_LAUNCH_B(1); break;
@@ -367,6 +383,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
     default: return hipErrorInvalidValue;
   }
 #undef PICP_LAUNCH_B
+#undef PICP_LAUNCH_BV
 #undef PICP_LAUNCH_B3
   return hipGetLastError();
 }

@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "picp_internal.h"
 
 namespace picp {
@@ -24,11 +26,43 @@ struct Cam {
   float maxx, maxy;  // cols-1, rows-1 (src/camera.h:31,33)
 };
 
+// Per-item math variant, fixed at launch (picp_variant): any K with the kernel weight chosen at
+// run time; the reference's pinhole K with outliers rejected (keep_outliers = false, as
+// icp_test runs it: every used item has weight exactly 1, so the weighted Jacobian IS the
+// Jacobian and no weight is formed); pinhole K with outliers kept (robust weight per item).
+#define PICP_V_GENERAL 0
+#define PICP_V_PINHOLE 1
+#define PICP_V_PINHOLE_KEEP 2
+
 struct Acc {
   float h[21];  // upper triangle of H, row-major (i<=j)
   float b[6];
-  float chi_in, chi_out, n_in, n_proj;
+  float chi_in, chi_out;
 };
+
+// n_in / n_proj of a wave, counted on the SCALAR unit: each item's inlier and projectable
+// predicates are already lane masks (v_cmp results), so a count is s_bcnt1 + s_add per mask,
+// issued beside the VALU work instead of as selects and adds in it.  Inside a divergent loop the
+// compiler keeps the counter per lane; a lane's copy then counts the items of every iteration
+// that lane ran, and lane 0 of a wave runs every iteration any lane of it runs (its items come
+// first), so wave_counts reads lane 0.
+struct Cnt {
+  unsigned n_in, n_proj;
+};
+
+__device__ __forceinline__ void cnt_add(Cnt& c, bool inl, bool valid) {
+  c.n_in += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(inl));
+  c.n_proj += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(valid));
+}
+
+// After wave_reduce32 (lane l holds the wave total of value l >> 1): the wave's counts, as the
+// float words of PICP_P_N_IN / PICP_P_N_PROJ (exact: a wave counts far fewer than 2^24 items).
+__device__ __forceinline__ float wave_counts(float wsum, int lane, const Cnt& c) {
+  const unsigned n_in = __builtin_amdgcn_readlane(c.n_in, 0);
+  const unsigned n_proj = __builtin_amdgcn_readlane(c.n_proj, 0);
+  wsum = ((lane >> 1) == PICP_P_N_IN) ? (float)n_in : wsum;
+  return ((lane >> 1) == PICP_P_N_PROJ) ? (float)n_proj : wsum;
+}
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -39,7 +73,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 struct Acc2 {
   f2 h[21];
   f2 b[6];
-  f2 chi_in, chi_out, n_in, n_proj;
+  f2 chi_in, chi_out;
 };
 
 __device__ __forceinline__ void acc2_zero(Acc2& a) {
@@ -47,10 +81,11 @@ __device__ __forceinline__ void acc2_zero(Acc2& a) {
   for (int i = 0; i < 21; ++i) a.h[i] = (f2){0.0f, 0.0f};
 #pragma unroll
   for (int i = 0; i < 6; ++i) a.b[i] = (f2){0.0f, 0.0f};
-  a.chi_in = a.chi_out = a.n_in = a.n_proj = (f2){0.0f, 0.0f};
+  a.chi_in = a.chi_out = (f2){0.0f, 0.0f};
 }
 
-// fold the two slots into the 32-term partial layout (picp_internal.h PICP_P_*)
+// fold the two slots into the 32-term partial layout (picp_internal.h PICP_P_*); the counts
+// are wave-level (Cnt, wave_counts)
 __device__ __forceinline__ void acc2_fold(const Acc2& a, float v[PICP_NPART]) {
 #pragma unroll
   for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i].x + a.h[i].y;
@@ -58,8 +93,8 @@ __device__ __forceinline__ void acc2_fold(const Acc2& a, float v[PICP_NPART]) {
   for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i].x + a.b[i].y;
   v[PICP_P_CHI_IN] = a.chi_in.x + a.chi_in.y;
   v[PICP_P_CHI_OUT] = a.chi_out.x + a.chi_out.y;
-  v[PICP_P_N_IN] = a.n_in.x + a.n_in.y;
-  v[PICP_P_N_PROJ] = a.n_proj.x + a.n_proj.y;
+  v[PICP_P_N_IN] = 0.0f;
+  v[PICP_P_N_PROJ] = 0.0f;
   v[31] = 0.0f;
 }
 
@@ -87,7 +122,7 @@ __device__ __forceinline__ bool rcp_safe(float x) {
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, float thr,
                                                bool keep, float x, float y, float z, float u,
-                                               float v, bool in_range, Acc& a) {
+                                               float v, bool in_range, Acc& a, Cnt& n) {
   float pc0, pc1, pc2, ph0, ph1, ph2, iz, e0, e1, chi;
   bool valid;
   {
@@ -121,8 +156,7 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
   const float w = inl ? 1.0f : lambda;
   a.chi_in += inl ? chi : 0.0f;
   a.chi_out += (valid && outlier) ? chi : 0.0f;
-  a.n_in += inl ? 1.0f : 0.0f;
-  a.n_proj += valid ? 1.0f : 0.0f;
+  cnt_add(n, inl, valid);
   // unused terms are zeroed by select before the Jacobian, so a skipped point (possibly
   // with an infinite iz) can never inject inf/NaN into H or b
   iz = use ? iz : 0.0f;
@@ -182,11 +216,14 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
 //   J1 = [0, a11, a12, a12 pc1 - a11 pc2, -a12 pc0, a11 pc0]
 // The structural zeros drop 12 of the 54 multiply-adds of H and b, and lambda = sqrt(thr/chi)
 // comes from v_rsq (it only weighs kept outliers, within the H/b tolerance): ~1/3 fewer VALU
-// instructions per correspondence than the general path.
+// instructions per correspondence than the general path.  KEEP (keep_outliers, compile time):
+// without it every used item has weight 1 and every other item has J = e = 0 (zeroed inputs),
+// so H and b take J itself -- bit-identical to multiplying by w in {0, 1}, 10 multiplies fewer.
+template <bool KEEP>
 __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, float thr,
-                                                   float inv_thr, bool keep, float x, float y,
+                                                   float inv_thr, float x, float y,
                                                    float z, float u, float v, bool in_range,
-                                                   Acc& a) {
+                                                   Acc& a, Cnt& n) {
   float pc0, pc1, pc2, ph0, ph1, iz, e0, e1, chi;
   bool valid, proj;
   {
@@ -208,23 +245,22 @@ __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, 
   }
   const bool outlier = chi > thr;
   const bool inl = valid & !outlier;
-  const bool use = inl | (valid & keep);
-  float w;
-  if (keep) {  // uniform (a kernel argument): the robust weight only when outliers are kept
-    w = use ? (inl ? 1.0f : __builtin_amdgcn_rsqf(chi * inv_thr)) : 0.0f;
-  } else {
-    w = inl ? 1.0f : 0.0f;
-  }
+  const bool use = inl | (valid & KEEP);
+  // the robust weight only when outliers are kept
+  const float w = KEEP ? (use ? (inl ? 1.0f : __builtin_amdgcn_rsqf(chi * inv_thr)) : 0.0f) : 1.0f;
   a.chi_in += inl ? chi : 0.0f;
   a.chi_out += (valid && outlier) ? chi : 0.0f;
-  a.n_in += inl ? 1.0f : 0.0f;
-  a.n_proj += valid ? 1.0f : 0.0f;
+  cnt_add(n, inl, valid);
   // A skipped point gets weight 0 and zeroed inputs, so it can never inject 0 * inf.  The
   // zeroing only matters for points whose J could be non-finite: ones that do not project, or
   // project from a depth under 1e-12.  A skipped point that projects from a larger depth
-  // (an outlier, a padding lane's copy) has a finite J, and fma(+-0, finite, h) == h exactly,
-  // so waves without a dangerous skipped point skip the 8 selects with bit-identical H and b.
-  if (!__all(use | (proj & (pc2 >= 1e-12f)))) {
+  // (an outlier, a padding lane's copy) has finite pc, ph and, with a finite chi, finite e: its
+  // J is exactly 0 once iz alone is zeroed, and fma(+-0, finite, h) == h exactly (the sums start
+  // at +0 and never become -0), so waves without a dangerous skipped point zero only iz, with
+  // bit-identical H and b.
+  if (__all(use | (proj & (pc2 >= 1e-12f) & (chi <= FLT_MAX)))) {
+    iz = use ? iz : 0.0f;
+  } else {
     iz = use ? iz : 0.0f;
     pc0 = use ? pc0 : 0.0f;
     pc1 = use ? pc1 : 0.0f;
@@ -253,8 +289,8 @@ __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, 
   float W0[6], W1[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    W0[i] = w * J0[i];
-    W1[i] = w * J1[i];
+    W0[i] = KEEP ? w * J0[i] : J0[i];
+    W1[i] = KEEP ? w * J1[i] : J1[i];
   }
   int k = 0;
 #pragma unroll
@@ -338,15 +374,16 @@ __device__ __forceinline__ void item_general(const Pose& T, const Cam& C, float 
 }
 
 // H += w (J0^T J0 + J1^T J1), b += w (J0^T e0 + J1^T e1) for both slots; SPARSE skips the
-// pinhole Jacobian's structural zeros J0[1] = J1[0] = 0
-template <bool SPARSE>
+// pinhole Jacobian's structural zeros J0[1] = J1[0] = 0; !WEIGHTED: w is 1 for every item whose
+// J is not zero (outliers rejected), so w is not applied
+template <bool SPARSE, bool WEIGHTED>
 __device__ __forceinline__ void acc2_normal(const f2 J0[6], const f2 J1[6], f2 e0, f2 e1, f2 w,
                                             Acc2& a) {
   f2 W0[6], W1[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    W0[i] = w * J0[i];
-    W1[i] = w * J1[i];
+    W0[i] = WEIGHTED ? w * J0[i] : J0[i];
+    W1[i] = WEIGHTED ? w * J1[i] : J1[i];
   }
   int k = 0;
 #pragma unroll
@@ -367,32 +404,52 @@ __device__ __forceinline__ void acc2_normal(const f2 J0[6], const f2 J1[6], f2 e
 }
 
 __device__ __forceinline__ void acc2_stats(f2 chi, bool inlA, bool inlB, bool validA, bool validB,
-                                           Acc2& a) {
+                                           Acc2& a, Cnt& n) {
   a.chi_in += (f2){inlA ? chi.x : 0.0f, inlB ? chi.y : 0.0f};
   a.chi_out += (f2){(validA & !inlA) ? chi.x : 0.0f, (validB & !inlB) ? chi.y : 0.0f};
-  a.n_in += (f2){inlA ? 1.0f : 0.0f, inlB ? 1.0f : 0.0f};
-  a.n_proj += (f2){validA ? 1.0f : 0.0f, validB ? 1.0f : 0.0f};
+  cnt_add(n, inlA, validA);
+  cnt_add(n, inlB, validB);
 }
 
 // A pair of correspondences, pinhole K: accumulate_pinhole's exact arithmetic with every
 // elementwise step packed (A in .x, B in .y).  Only the correctly rounded reciprocal, the
 // compares and the selects stay per item.  Contraction is off exactly where the oracle has it
 // off (gate and Jacobian), so both items are bit-identical to the scalar path.
+// The camera-frame depth of a pair, in the exact operation order of accumulate_pinhole2 (so the
+// compiler shares it): callers check a whole section of pairs for the fast reciprocal at once.
+__device__ __forceinline__ f2 pair_depth(const Pose& T, f2 x, f2 y, f2 z) {
+#pragma clang fp contract(off)
+  return ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;  // src/camera.h:26, row 2
+}
+
+__device__ __forceinline__ bool pair_rcp_safe(const Pose& T, f2 x, f2 y, f2 z) {
+  const f2 d = pair_depth(T, x, y, z);
+  return rcp_safe(d.x) & rcp_safe(d.y);
+}
+
+// The reciprocal of the depth (ph2 == pc2 exactly): RCP_CHECK decides per pair by a wave vote;
+// RCP_FAST: the caller's vote found every depth of the section inside rcp_safe's range (rcp_rn,
+// exhaustively verified); RCP_DIV: the IEEE division.
+#define RCP_CHECK 0
+#define RCP_FAST 1
+#define RCP_DIV 2
+
+template <bool KEEP, int RCP = RCP_CHECK>
 __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C, float thr,
-                                                    float inv_thr, bool keep, f2 x, f2 y, f2 z,
-                                                    f2 u, f2 v, bool inA, bool inB, Acc2& a) {
+                                                    float inv_thr, f2 x, f2 y, f2 z,
+                                                    f2 u, f2 v, bool inA, bool inB, Acc2& a, Cnt& n) {
   f2 pc0, pc1, pc2, ph0, ph1, iz, e0, e1, chi;
   bool validA, validB;
   {
 #pragma clang fp contract(off)
     pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;  // src/camera.h:26
     pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
-    pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
+    pc2 = pair_depth(T, x, y, z);
     ph0 = C.k00 * pc0 + C.k02 * pc2;  // src/camera.h:29 without the zero terms
     ph1 = C.k11 * pc1 + C.k12 * pc2;
     // ph2 == pc2 exactly; the correctly rounded reciprocal per item (rcp_rn, exhaustively
     // verified), the IEEE division only when a lane of the wave holds an extreme value
-    if (__all(rcp_safe(pc2.x) & rcp_safe(pc2.y))) {
+    if (RCP == RCP_FAST || (RCP == RCP_CHECK && __all(rcp_safe(pc2.x) & rcp_safe(pc2.y)))) {
       iz.x = rcp_rn(pc2.x);
       iz.y = rcp_rn(pc2.y);
     } else {
@@ -412,11 +469,14 @@ __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C,
   }
   const bool outA = chi.x > thr, outB = chi.y > thr;
   const bool inlA = validA & !outA, inlB = validB & !outB;
-  const bool useA = inlA | (validA & keep), useB = inlB | (validB & keep);
-  const f2 q = chi * inv_thr;
-  const f2 w = {useA ? (inlA ? 1.0f : __builtin_amdgcn_rsqf(q.x)) : 0.0f,
-                useB ? (inlB ? 1.0f : __builtin_amdgcn_rsqf(q.y)) : 0.0f};
-  acc2_stats(chi, inlA, inlB, validA, validB, a);
+  const bool useA = inlA | (validA & KEEP), useB = inlB | (validB & KEEP);
+  f2 w = {1.0f, 1.0f};
+  if constexpr (KEEP) {  // the robust weight only when outliers are kept
+    const f2 q = chi * inv_thr;
+    w = (f2){useA ? (inlA ? 1.0f : __builtin_amdgcn_rsqf(q.x)) : 0.0f,
+             useB ? (inlB ? 1.0f : __builtin_amdgcn_rsqf(q.y)) : 0.0f};
+  }
+  acc2_stats(chi, inlA, inlB, validA, validB, a, n);
   // a skipped item gets weight 0 and finite inputs, so it can never inject inf/NaN.  (Skipping
   // these selects for waves of projectable items, as accumulate_pinhole does, measured 1-4 %
   // slower here: the branches split the unrolled pairs' straight-line schedule.)
@@ -440,45 +500,81 @@ __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C,
     J1[4] = -(a12 * pc0);
     J1[5] = a11 * pc0;
   }
-  acc2_normal<true>(J0, J1, e0, e1, w, a);
+  acc2_normal<true, KEEP>(J0, J1, e0, e1, w, a);
 }
 
 // A pair of correspondences, general K: per-item math (item_general), packed accumulation.
 __device__ __forceinline__ void accumulate_general2(const Pose& T, const Cam& C, float thr, bool keep,
                                                     f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
-                                                    bool inB, Acc2& a) {
+                                                    bool inB, Acc2& a, Cnt& n) {
   Item A, B;
   item_general(T, C, thr, keep, x.x, y.x, z.x, u.x, v.x, inA, A);
   item_general(T, C, thr, keep, x.y, y.y, z.y, u.y, v.y, inB, B);
-  acc2_stats((f2){A.chi, B.chi}, A.inl, B.inl, A.valid, B.valid, a);
+  acc2_stats((f2){A.chi, B.chi}, A.inl, B.inl, A.valid, B.valid, a, n);
   f2 J0[6], J1[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     J0[i] = (f2){A.J0[i], B.J0[i]};
     J1[i] = (f2){A.J1[i], B.J1[i]};
   }
-  acc2_normal<false>(J0, J1, (f2){A.e0, B.e0}, (f2){A.e1, B.e1}, (f2){A.w, B.w}, a);
+  acc2_normal<false, true>(J0, J1, (f2){A.e0, B.e0}, (f2){A.e1, B.e1}, (f2){A.w, B.w}, a);
 }
 
-template <int PH>
+// PH: the per-item variant (PICP_V_*); keep is read only by the general variant; RCP: how the
+// pinhole variants take the reciprocal (RCP_*)
+template <int PH, int RCP = RCP_CHECK>
 __device__ __forceinline__ void accumulate2(const Pose& T, const Cam& C, float thr, float inv_thr,
                                             bool keep, f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
-                                            bool inB, Acc2& a) {
-  if constexpr (PH)
-    accumulate_pinhole2(T, C, thr, inv_thr, keep, x, y, z, u, v, inA, inB, a);
+                                            bool inB, Acc2& a, Cnt& n) {
+  if constexpr (PH == PICP_V_GENERAL)
+    accumulate_general2(T, C, thr, keep, x, y, z, u, v, inA, inB, a, n);
   else
-    accumulate_general2(T, C, thr, keep, x, y, z, u, v, inA, inB, a);
+    accumulate_pinhole2<PH == PICP_V_PINHOLE_KEEP, RCP>(T, C, thr, inv_thr, x, y, z, u, v, inA, inB, a, n);
 }
 
-// one correspondence with the camera path chosen at compile time (PH = pinhole K)
+// NPT register-resident items per lane (item k at lane + k * stride) as pairs (k, k + 1) (NPT == 1:
+// slot B repeats item 0, masked), with ONE wave vote on the fast reciprocal for the whole set
+// instead of one per pair: the pairs then run as one straight-line block (a vote per pair split
+// them into blocks, so every per-item predicate crossing the block edge was kept as a 0/1 VGPR and
+// compared again, and the masks' scalar registers spilled).
+template <int PH, int NPT>
+__device__ __forceinline__ void accumulate_regs(const Pose& T, const Cam& C, float thr, float inv_thr,
+                                                bool keep, const float* xs, const float* ys,
+                                                const float* zs, const float* us, const float* vs,
+                                                int first, int stride, int n, Acc2& a, Cnt& cnt) {
+  bool fast = true;
+  if constexpr (PH != PICP_V_GENERAL) {
+#pragma unroll
+    for (int k = 0; k < NPT; k += 2) {
+      const int k1 = (k + 1 < NPT) ? k + 1 : k;
+      fast &= pair_rcp_safe(T, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]}, (f2){zs[k], zs[k1]});
+    }
+  }
+  auto run = [&](auto rcp) {
+#pragma unroll
+    for (int k = 0; k < NPT; k += 2) {
+      const int k1 = (k + 1 < NPT) ? k + 1 : k;
+      accumulate2<PH, decltype(rcp)::value>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]},
+                                            (f2){zs[k], zs[k1]}, (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]},
+                                            first + k * stride < n, k + 1 < NPT && first + (k + 1) * stride < n,
+                                            a, cnt);
+    }
+  };
+  if (PH == PICP_V_GENERAL || __all(fast))
+    run(std::integral_constant<int, RCP_FAST>());
+  else
+    run(std::integral_constant<int, RCP_DIV>());
+}
+
+// one correspondence with the variant chosen at compile time
 template <int PH>
 __device__ __forceinline__ void accumulate(const Pose& T, const Cam& C, float thr, float inv_thr,
                                            bool keep, float x, float y, float z, float u,
-                                           float v, bool in_range, Acc& a) {
-  if constexpr (PH)
-    accumulate_pinhole(T, C, thr, inv_thr, keep, x, y, z, u, v, in_range, a);
+                                           float v, bool in_range, Acc& a, Cnt& n) {
+  if constexpr (PH == PICP_V_GENERAL)
+    accumulate_one(T, C, thr, keep, x, y, z, u, v, in_range, a, n);
   else
-    accumulate_one(T, C, thr, keep, x, y, z, u, v, in_range, a);
+    accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
 }
 
 __host__ __device__ inline bool is_pinhole(const float K[9]) {  // column-major K
@@ -494,6 +590,13 @@ inline bool picp_use_pinhole(const float K[9]) {
     return e && atoi(e) != 0;
   }();
   return !force_general && picp::is_pinhole(K);
+}
+
+// launch-time per-item variant (PICP_V_*): the camera path, and for the pinhole path whether
+// outliers are kept (a compile-time weight)
+inline int picp_variant(const float K[9], int keep_outliers) {
+  if (!picp_use_pinhole(K)) return PICP_V_GENERAL;
+  return keep_outliers ? PICP_V_PINHOLE_KEEP : PICP_V_PINHOLE;
 }
 
 namespace picp {

@@ -240,6 +240,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
 
   Acc2 a;
   acc2_zero(a);
+  Cnt nc = {0u, 0u};  // the wave's counts; the loop is divergent at the tail: lane 0's copy is the total
   for (int c = c0; c < count; c += RING * STEP) {
 #pragma unroll
     for (int sl = 0; sl < RING; ++sl) {
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
           accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){bx[sl][k], bx[sl][k + 1]},
                           (f2){by[sl][k], by[sl][k + 1]}, (f2){bz[sl][k], bz[sl][k + 1]},
                           (f2){bu[sl][k], bu[sl][k + 1]}, (f2){bv[sl][k], bv[sl][k + 1]},
-                          ps + k * ISTRIDE < count, ps + (k + 1) * ISTRIDE < count, a);
+                          ps + k * ISTRIDE < count, ps + (k + 1) * ISTRIDE < count, a, nc);
         const int cn = cs + RING * STEP;
         if (cn < count) load_step(phys(cn), bx[sl], by[sl], bz[sl], bu[sl], bv[sl]);
       }
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
   float v[PICP_NPART];
   acc2_fold(a, v);
   const int lane = tid & 63, wave = tid >> 6;
-  const float wsum = wave_reduce32(v, lane);
+  const float wsum = wave_counts(wave_reduce32(v, lane), lane, nc);
   if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
   __syncthreads();
   // publish: lane t < 16 of wave 0 stores partial floats (2t, 2t+1) as one write-through
@@ -361,17 +362,22 @@ extern "C" hipError_t picp_launch_round(hipStream_t stream, int grid, int vec, c
   const char* fwd = getenv("PICP_SWEEP_FORWARD");  // read per launch: graphs capture it
   const bool forward_only = fwd && atoi(fwd) != 0;
   const int rev = (!forward_only && (j & 1)) ? 1 : 0;
-  const bool ph = picp_use_pinhole(args->K);
+  const int var = picp_variant(args->K, args->keep_outliers);
 #define PICP_LAUNCH_R(VEC, PH)                                                                        \
   hipLaunchKernelGGL((picp_round_kernel<VEC, PH>), dim3(grid), dim3(PICP_BLOCK), 0, stream, X, Y, Z, U, \
                      V, *args, probs, blkinfo, st_in, st_out, part, tickets, j, rev)
+#define PICP_LAUNCH_RV(VEC)                                                        \
+  if (var == PICP_V_PINHOLE) PICP_LAUNCH_R(VEC, PICP_V_PINHOLE);                   \
+  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_R(VEC, PICP_V_PINHOLE_KEEP);    \
+  else PICP_LAUNCH_R(VEC, PICP_V_GENERAL)
   if (vec == 4) {
-    if (ph) PICP_LAUNCH_R(4, 1); else PICP_LAUNCH_R(4, 0);
+    PICP_LAUNCH_RV(4);
   } else if (vec == 1) {
-    if (ph) PICP_LAUNCH_R(1, 1); else PICP_LAUNCH_R(1, 0);
+    PICP_LAUNCH_RV(1);
   } else {
     return hipErrorInvalidValue;
   }
+#undef PICP_LAUNCH_RV
 #undef PICP_LAUNCH_R
   return hipGetLastError();
 }

@@ -147,34 +147,31 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
     float v[PICP_NPART];
+    Cnt nc = {0u, 0u};  // the wave's n_in / n_proj (scalar unit)
     if constexpr (NPT == 1) {  // one item per lane: the scalar path (latency-bound C2 frames)
       Acc a;
 #pragma unroll
       for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
 #pragma unroll
       for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
-      a.chi_in = a.chi_out = a.n_in = a.n_proj = 0.0f;
-      accumulate<PH>(T, C, thr, inv_thr, keep, xs[0], ys[0], zs[0], us[0], vs[0], tid < count, a);
+      a.chi_in = a.chi_out = 0.0f;
+      accumulate<PH>(T, C, thr, inv_thr, keep, xs[0], ys[0], zs[0], us[0], vs[0], tid < count, a, nc);
 #pragma unroll
       for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
 #pragma unroll
       for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
       v[PICP_P_CHI_IN] = a.chi_in;
       v[PICP_P_CHI_OUT] = a.chi_out;
-      v[PICP_P_N_IN] = a.n_in;
-      v[PICP_P_N_PROJ] = a.n_proj;
+      v[PICP_P_N_IN] = 0.0f;
+      v[PICP_P_N_PROJ] = 0.0f;
       v[31] = 0.0f;
     } else {  // pairs of register-resident items, packed (accumulate2)
       Acc2 a;
       acc2_zero(a);
-#pragma unroll
-      for (int k = 0; k < NPT; k += 2)
-        accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k + 1]}, (f2){ys[k], ys[k + 1]},
-                        (f2){zs[k], zs[k + 1]}, (f2){us[k], us[k + 1]}, (f2){vs[k], vs[k + 1]},
-                        tid + k * PICP_PBLOCK < count, tid + (k + 1) * PICP_PBLOCK < count, a);
+      accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, PICP_PBLOCK, count, a, nc);
       acc2_fold(a, v);
     }
-    const float wsum = wave_reduce32(v, lane);
+    const float wsum = wave_counts(wave_reduce32(v, lane), lane, nc);
     if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
     __syncthreads();
     if (tid < PICP_NPART) {
@@ -325,20 +322,37 @@ extern "C" hipError_t picp_debug_pstamps(unsigned long long* out, size_t n_words
 // ------------------------------- host launch wrapper -------------------------------
 extern "C" int picp_persistent_block(void) { return PICP_PBLOCK; }
 
+template <int N>
+static const void* persistent_kernel_n(int var) {
+  switch (var) {
+    case PICP_V_PINHOLE: return (const void*)picp_persistent_kernel<N, PICP_V_PINHOLE>;
+    case PICP_V_PINHOLE_KEEP: return (const void*)picp_persistent_kernel<N, PICP_V_PINHOLE_KEEP>;
+    default: return (const void*)picp_persistent_kernel<N, PICP_V_GENERAL>;
+  }
+}
+
 // Blocks of the persistent variant for (npt, K) one CU holds at once (registers, LDS, waves).
 // Its blocks hand rounds to each other, so the host launches it only when grid <= this x CUs.
 extern "C" hipError_t picp_persistent_occupancy(int npt, const float K[9], int* blocks_per_cu) {
   if (!blocks_per_cu) return hipErrorInvalidValue;
-  const bool ph = picp_use_pinhole(K);
-  const void* fn = nullptr;
-  switch (npt) {
-    case 1: fn = ph ? (const void*)picp_persistent_kernel<1, 1> : (const void*)picp_persistent_kernel<1, 0>; break;
-    case 2: fn = ph ? (const void*)picp_persistent_kernel<2, 1> : (const void*)picp_persistent_kernel<2, 0>; break;
-    case 4: fn = ph ? (const void*)picp_persistent_kernel<4, 1> : (const void*)picp_persistent_kernel<4, 0>; break;
-    case 8: fn = ph ? (const void*)picp_persistent_kernel<8, 1> : (const void*)picp_persistent_kernel<8, 0>; break;
-    default: return hipErrorInvalidValue;
+  // the smaller of the two pinhole variants: keep_outliers is a per-solve argument
+  int best = -1;
+  for (int keep = 0; keep < 2; ++keep) {
+    const void* fn = nullptr;
+    switch (npt) {
+      case 1: fn = persistent_kernel_n<1>(picp_variant(K, keep)); break;
+      case 2: fn = persistent_kernel_n<2>(picp_variant(K, keep)); break;
+      case 4: fn = persistent_kernel_n<4>(picp_variant(K, keep)); break;
+      case 8: fn = persistent_kernel_n<8>(picp_variant(K, keep)); break;
+      default: return hipErrorInvalidValue;
+    }
+    int occ = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, PICP_PBLOCK, 0);
+    if (e != hipSuccess) return e;
+    best = (best < 0 || occ < best) ? occ : best;
   }
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, PICP_PBLOCK, 0);
+  *blocks_per_cu = best;
+  return hipSuccess;
 }
 
 extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int npt, const float* X,
@@ -349,14 +363,14 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              unsigned int* err, unsigned int* tagbase,
                                              unsigned long long timeout_ticks) {
   if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
-  const bool ph = picp_use_pinhole(args->K);
-#define PICP_LAUNCH_P(N)                                                                                 \
-  if (ph)                                                                                                \
-    hipLaunchKernelGGL((picp_persistent_kernel<N, 1>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
-                       U, V, *args, st_in, st_out, gpart, gpose, err, tagbase, timeout_ticks);                   \
-  else                                                                                                   \
-    hipLaunchKernelGGL((picp_persistent_kernel<N, 0>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
-                       U, V, *args, st_in, st_out, gpart, gpose, err, tagbase, timeout_ticks)
+  const int var = picp_variant(args->K, args->keep_outliers);
+#define PICP_LAUNCH_PV(N, PV)                                                                           \
+  hipLaunchKernelGGL((picp_persistent_kernel<N, PV>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
+                     U, V, *args, st_in, st_out, gpart, gpose, err, tagbase, timeout_ticks)
+#define PICP_LAUNCH_P(N)                                                            \
+  if (var == PICP_V_PINHOLE) PICP_LAUNCH_PV(N, PICP_V_PINHOLE);                     \
+  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_PV(N, PICP_V_PINHOLE_KEEP);      \
+  else PICP_LAUNCH_PV(N, PICP_V_GENERAL)
   switch (npt) {
     case 1: PICP_LAUNCH_P(1); break;
     case 2: PICP_LAUNCH_P(2); break;
@@ -365,5 +379,6 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
     default: return hipErrorInvalidValue;
   }
 #undef PICP_LAUNCH_P
+#undef PICP_LAUNCH_PV
   return hipGetLastError();
 }
