@@ -4,8 +4,9 @@
 // The first NPT*PICP_BBLOCK correspondences of a problem are loaded once into registers (NPT
 // per lane); any remainder is re-read every round (two per lane per step, L2/MALL-resident
 // after the first round).  Every round is: linearize in registers -> wave64 reduction (permlane/DPP) -> LDS
-// combine of the 8 waves -> one lane finishes the round (fp32 LDL^T, Rx*Ry*Rz update,
-// convergence; picp_device.h) -> barrier.  No inter-workgroup communication at all, no launch
+// combine of the 8 waves -> wave 0 finishes the round (fp32 LDL^T, Rx*Ry*Rz update,
+// convergence; picp_device.h finish_round_pose, every lane the same values, the loop state in
+// registers) -> barrier.  No inter-workgroup communication at all, no launch
 // per round and no HBM re-read per round: a batch of frames is bound by VALU issue, not by
 // hand-off latency or HBM.  Ragged batches read (offset, n) from the problem
 // table.
@@ -63,7 +64,8 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
     unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks) {
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
-  __shared__ float s_wave[BS / 64][PICP_NPART];
+  // wave sums, term-major: the lane combining term e reads its BS/64 wave sums as 16-B loads
+  __shared__ __attribute__((aligned(16))) float s_wave[PICP_NPART][BS / 64];
   __shared__ float s_tot[PICP_NPART];  // the totals as finish_round_f words (total_word)
   __shared__ float s_pose[12];
   __shared__ int s_done;
@@ -159,6 +161,9 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
   const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
 
+  // the icp_test loop state a round reads: the pose (s_pose, every wave) and chi_prev (wave 0,
+  // which finishes the rounds, keeps it in a register)
+  float chi_prev = FLT_MAX;  // exec/icp_test.cpp:89
   for (int round = 1; !s_done; ++round) {
     BSTAMP(0);
     Pose T;
@@ -190,14 +195,25 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     BSTAMP(1);
     acc2_fold(a, v);
     const float wsum = wave_counts(wave_reduce32(v, lane), lane, (Cnt){nr.n_in + nd.n_in, nr.n_proj + nd.n_proj});
-    if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;
+    if ((lane & 1) == 0) s_wave[lane >> 1][wave] = wsum;
     BSTAMP(2);
     __syncthreads();
     BSTAMP(3);
-    if (tid < PICP_NPART) {  // fixed-order combine of the 8 waves, one lane per term
-      double t = 0.0;
+    // the finishing wave's pose, re-read here (three 16-B LDS loads, landing during the combine)
+    // rather than kept live through the linearize, where it spilled; s_pose changes only after
+    // this round's finish
+    float pr[9], pt[3];
 #pragma unroll
-      for (int w = 0; w < BS / 64; ++w) t += (double)s_wave[w][tid];
+    for (int i = 0; i < 9; ++i) pr[i] = s_pose[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pt[i] = s_pose[9 + i];
+    if (tid < PICP_NPART) {  // fixed-order combine of the 8 waves, one lane per term
+      float ws[BS / 64];  // every load issued before the first add (one LDS wait)
+#pragma unroll
+      for (int w = 0; w < BS / 64; ++w) ws[w] = s_wave[tid][w];
+      double t = (double)ws[0];
+#pragma unroll
+      for (int w = 1; w < BS / 64; ++w) t += (double)ws[w];
       if (split > 1) {
         // publish {round, hi}, {round, lo}; poll the partners'; add the parts in part order
         const float hi = (float)t, lo = (float)(t - (double)hi);
@@ -250,19 +266,18 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     // a wave barrier orders them, the other waves wait at the block barrier after the solve
     __builtin_amdgcn_wave_barrier();
     BSTAMP(4);
-    if (tid == 0) {
-      float tw[PICP_NPART];
+    if (wave == 0) {  // the wave finishes the round (every lane the same values, state in registers)
+      RoundOut o;
+      finish_round_pose(A, s_tot, round, pr, pt, chi_prev, o);
+      if (s_tmo) o.done = 1;  // a partner wait timed out: stop (the host reports the error)
+      if (lane == 0) {
 #pragma unroll
-      for (int i = 0; i < PICP_NPART; ++i) tw[i] = s_tot[i];
-      PicpState ns;
-      finish_round_f(A, s_st, tw, round, ns);
-      if (s_tmo) ns.done = 1;  // a partner wait timed out: stop (the host reports the error)
-      s_st = ns;
+        for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
-      s_done = ns.done;
+        for (int i = 0; i < 3; ++i) s_pose[9 + i] = pt[i];
+        s_done = o.done;
+        if (o.done) store_state(&s_st, pr, pt, chi_prev, o, round);
+      }
     }
     BSTAMP(5);
     last_round = round;

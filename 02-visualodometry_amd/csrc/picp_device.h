@@ -656,70 +656,86 @@ __device__ __forceinline__ float rcp32(float d) {
   return (fabsf(d) > FLT_MIN) ? r : 0.0f;
 }
 
-// Damped normal equations -> dx.  float32 LDL^T, the precision the reference solves in
-// (Matrix6f::ldlt, src/picp_solver.cpp:102); H and b arrive as exact double sums.  Plain LDL^T
-// without Eigen's diagonal pivoting (H + damping*I is SPD: pivoting only changes rounding).
-// Fully unrolled: registers only, one lane.
-__device__ __forceinline__ void ldlt6_solve(float A[6][6], const float rhs[6], float x[6]) {
-  float L[6][6], D[6], iD[6];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    float d = A[j][j];
-    float LD[6];
-#pragma unroll
-    for (int k = 0; k < j; ++k) {
-      LD[k] = L[j][k] * D[k];
-      d = fmaf(-LD[k], L[j][k], d);
-    }
-    D[j] = d;
-    iD[j] = rcp32(d);
-#pragma unroll
-    for (int i = j + 1; i < 6; ++i) {
-      float s = A[i][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) s = fmaf(-L[i][k], LD[k], s);
-      L[i][j] = s * iD[j];
-    }
-  }
-  float y[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    float s = rhs[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) s = fmaf(-L[i][k], y[k], s);
-    y[i] = s;
-  }
-#pragma unroll
-  for (int i = 0; i < 6; ++i) y[i] *= iD[i];
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    float s = y[i];
-#pragma unroll
-    for (int k = i + 1; k < 6; ++k) s = fmaf(-L[k][i], x[k], s);
-    x[i] = s;
-  }
+// Damped normal equations -> dx, in float32, the precision the reference solves in
+// (Matrix6f::ldlt, src/picp_solver.cpp:102); H and b arrive as exact double sums.  LDL^T without
+// pivoting, by Gaussian elimination on the LOWER triangle (H + damping*I is SPD: Eigen's diagonal
+// pivoting only changes rounding): step j scales column j by 1/d_j and updates the trailing
+// lower triangle; the back substitution reads U = D L^T from the lower entries (symmetry).  Pivot
+// reciprocals are the hardware v_rcp_f32 (<= 1 ulp).  A pivot with |d| <= FLT_MIN gives 1/d = 0,
+// Eigen's zero-pivot rule for float; that test is kept off the pivot chain (a flag, and the rare
+// flagged system is solved again with the guard in the chain).  One lane, registers only, every
+// index compile-time: the per-round critical path of every kernel (tools/ubench/parts_ubench).
+// Row r of the system is read from the converted totals tw (total_word: damping folded into the
+// diagonal, -b), upper triangle row-major.
+__device__ __forceinline__ int tri_index(int r, int c) {  // upper-triangle slot of (min, max)
+  const int lo = r < c ? r : c, hi = r < c ? c : r;
+  return PICP_P_H + lo * (11 - lo) / 2 + hi;
 }
 
-// sin/cos of a GN increment angle.  Increments are small, so the float Taylor series (exact to
-// float rounding for |a| <= 1/16: next term a^9/9! < 1e-16) avoids sincosf's range reduction
-// on the single-lane critical path; larger angles take the libm path.
-__device__ __forceinline__ void small_sincos(float a, float* s, float* c) {
-  if (fabsf(a) <= 0.0625f) {
-    const float a2 = a * a;
-    *s = a * fmaf(a2, fmaf(a2, fmaf(a2, -1.0f / 5040.0f, 1.0f / 120.0f), -1.0f / 6.0f), 1.0f);
-    *c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 1.0f / 40320.0f, -1.0f / 720.0f), 1.0f / 24.0f), -0.5f), 1.0f);
-  } else {
-    sincosf(a, s, c);
+template <bool GUARD>
+__device__ __forceinline__ bool ldl6_solve(const float* tw, float dx[6]) {
+  float a[6][6], rhs[6], id[6];
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int c = 0; c <= i; ++c) a[i][c] = tw[tri_index(c, i)];
+    rhs[i] = tw[PICP_P_B + i];
   }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const float d = a[j][j];
+    float inv = __builtin_amdgcn_rcpf(d);
+    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
+    else bad |= !(fabsf(d) > FLT_MIN);
+    id[j] = inv;
+    float f[6];
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) f[i] = a[i][j] * inv;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+#pragma unroll
+      for (int c = j + 1; c <= i; ++c) a[i][c] = fmaf(-f[i], a[c][j], a[i][c]);
+      rhs[i] = fmaf(-f[i], rhs[j], rhs[i]);
+    }
+  }
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    const float x = rhs[k] * id[k];
+    dx[k] = x;
+#pragma unroll
+    for (int i = 0; i < k; ++i) rhs[i] = fmaf(-a[k][i], x, rhs[i]);
+  }
+  return bad;
+}
+
+__device__ __forceinline__ void ldl6_solve(const float* tw, float dx[6]) {
+  if (ldl6_solve<false>(tw, dx)) ldl6_solve<true>(tw, dx);  // a (near-)zero pivot: rare
+}
+
+// sin/cos of GN increment angles.  Increments are small, so the float Taylor series (exact to
+// float rounding for |a| <= 1/16: next term a^9/9! < 1e-16) avoids sincosf's range reduction
+// on the critical path; ONE test for the three angles keeps the common case straight-line (three
+// independent polynomial chains); larger angles take the libm path.
+__device__ __forceinline__ void taylor_sincos(float a, float* s, float* c) {
+  const float a2 = a * a;
+  *s = a * fmaf(a2, fmaf(a2, fmaf(a2, -1.0f / 5040.0f, 1.0f / 120.0f), -1.0f / 6.0f), 1.0f);
+  *c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 1.0f / 40320.0f, -1.0f / 720.0f), 1.0f / 24.0f), -0.5f), 1.0f);
 }
 
 // src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
 // src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
 __device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
   float sa, ca, sb, cb, sc, cc;
-  small_sincos(dx[3], &sa, &ca);
-  small_sincos(dx[4], &sb, &cb);
-  small_sincos(dx[5], &sc, &cc);
+  if (fabsf(dx[3]) <= 0.0625f && fabsf(dx[4]) <= 0.0625f && fabsf(dx[5]) <= 0.0625f) {
+    taylor_sincos(dx[3], &sa, &ca);
+    taylor_sincos(dx[4], &sb, &cb);
+    taylor_sincos(dx[5], &sc, &cc);
+  } else {
+    sincosf(dx[3], &sa, &ca);
+    sincosf(dx[4], &sb, &cb);
+    sincosf(dx[5], &sc, &cc);
+  }
   // Rd = Rx(a)*Ry(b)*Rz(c) in closed form: the same products and sums as the 3x3 products
   // of src/defs.h:133 with their structural zeros and ones folded away (x*1 = x, x+0 = x).
   const float sasb = sa * sb, casb = ca * sb;
@@ -759,66 +775,88 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
 // diagonal (src/picp_solver.cpp:96), -b, chi_in, chi_out as float, n_in and n_proj as int bits.
 __device__ __forceinline__ float total_word(const PicpArgs& A, int e, double t) {
   const bool diag = (e == 0) | (e == 6) | (e == 11) | (e == 15) | (e == 18) | (e == 20);
-  if (e < PICP_P_B) return (float)(t + (diag ? (double)A.damping : 0.0));
-  if (e < PICP_P_CHI_IN) return (float)(-t);
-  if (e < PICP_P_N_IN) return (float)t;
-  if (e < 31) return __int_as_float((int32_t)t);
-  return 0.0f;
+  // straight-line selects (lane e converts total e: branches would serialise the wave)
+  const double h = t + (diag ? (double)A.damping : 0.0);
+  const double d = (e < PICP_P_B) ? h : ((e < PICP_P_CHI_IN) ? -t : t);
+  const float f = (float)d;
+  const float c = __int_as_float((int32_t)t);
+  return (e < PICP_P_N_IN) ? f : ((e < 31) ? c : 0.0f);
 }
 
-// Finish round (j-1) of a problem from its converted totals (total_word): damping is already
-// in, so this is the min-inlier check, the 6x6 solve, the update and the icp_test loop state.
-// Runs in one lane (or redundantly in several); everything is indexed by compile-time constants.
-__device__ __forceinline__ void finish_round_f(const PicpArgs& A, const PicpState& s,
-                                               const float* tw, int j, PicpState& ns) {
-  // field-wise, padding zeroed: a whole-struct copy of an LDS state kept its 44-byte tail in a
-  // scratch alloca (SROA cannot split the memcpy), a round trip on every round's critical path
-#pragma unroll
-  for (int i = 0; i < 9; ++i) ns.R[i] = s.R[i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) ns.t[i] = s.t[i];
-  ns.chi_prev = s.chi_prev;
-  ns.done = s.done;
-  ns.ok = s.ok;
-  ns.converged = s.converged;
-#pragma unroll
-  for (int i = 0; i < 11; ++i) ns.pad[i] = 0;
-  ns.chi_in = tw[PICP_P_CHI_IN];
-  ns.chi_out = tw[PICP_P_CHI_OUT];
-  ns.n_in = __float_as_int(tw[PICP_P_N_IN]);
-  ns.n_proj = __float_as_int(tw[PICP_P_N_PROJ]);
-  ns.rounds = j;
-  float H[6][6];
-  int k = 0;
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int c = r; c < 6; ++c) {
-      H[r][c] = tw[PICP_P_H + k];  // :96 (damping folded in by total_word)
-      H[c][r] = tw[PICP_P_H + k];
-      ++k;
-    }
-  if (ns.n_in < A.min_inliers) {  // src/picp_solver.cpp:97-100
-    ns.ok = 0;
-    ns.done = 1;
+// What a round leaves besides the pose: the state fields no later round reads.
+struct RoundOut {
+  float chi_in, chi_out;
+  int32_t n_in, n_proj, ok, done, converged;
+};
+
+// Finish round j of a problem from its converted totals (total_word: damping already in): the
+// min-inlier check, the 6x6 solve, the update and the icp_test loop rule.  The loop state a round
+// reads -- the pose R (column-major) / t and chi_prev -- is carried in registers by the finishing
+// wave (every lane computes the same values; no LDS state round trip on the critical path).
+// tw may be LDS.
+__device__ __forceinline__ void finish_round_pose(const PicpArgs& A, const float* tw, int j, float R[9],
+                                                  float t[3], float& chi_prev, RoundOut& o) {
+  o.chi_in = tw[PICP_P_CHI_IN];
+  o.chi_out = tw[PICP_P_CHI_OUT];
+  o.n_in = __float_as_int(tw[PICP_P_N_IN]);
+  o.n_proj = __float_as_int(tw[PICP_P_N_PROJ]);
+  o.converged = 0;  // a converged loop is done: no round runs after it
+  if (o.n_in < A.min_inliers) {  // src/picp_solver.cpp:97-100
+    o.ok = 0;
+    o.done = 1;
     return;
   }
-  float nb[6], dx[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) nb[r] = tw[PICP_P_B + r];
-  ldlt6_solve(H, nb, dx);        // :102
-  apply_update(dx, ns.R, ns.t);  // :103
-  ns.ok = 1;
+  float dx[6];
+  ldl6_solve(tw, dx);      // :96 (damping folded in by total_word), :102
+  apply_update(dx, R, t);  // :103
+  o.ok = 1;
+  o.done = 0;
   // exec/icp_test.cpp:99-106
-  const float prev = s.chi_prev, cur = ns.chi_in;
+  const float prev = chi_prev, cur = o.chi_in;
   const float rel = (prev > 1e-10f) ? fabsf(prev - cur) / prev : 0.0f;
   if (rel < A.conv_eps) {
-    ns.converged = 1;
-    ns.done = 1;
+    o.converged = 1;
+    o.done = 1;
   } else {
-    ns.chi_prev = cur;
+    chi_prev = cur;
   }
-  if (j >= A.max_rounds) ns.done = 1;
+  if (j >= A.max_rounds) o.done = 1;
+}
+
+// The 128-byte state after round j, written field by field (padding zeroed): a whole-struct copy
+// from a local goes through a scratch alloca (SROA cannot split the memcpy).  dst: LDS or global.
+template <typename S>
+__device__ __forceinline__ void store_state(S* dst, const float R[9], const float t[3], float chi_prev,
+                                            const RoundOut& o, int j) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) dst->R[i] = R[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) dst->t[i] = t[i];
+  dst->chi_prev = chi_prev;
+  dst->chi_in = o.chi_in;
+  dst->chi_out = o.chi_out;
+  dst->n_in = o.n_in;
+  dst->n_proj = o.n_proj;
+  dst->rounds = j;
+  dst->done = o.done;
+  dst->ok = o.ok;
+  dst->converged = o.converged;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) dst->pad[i] = 0;
+}
+
+// finish_round_pose on a stored state (the multi-launch round kernel: one lane).
+__device__ __forceinline__ void finish_round_f(const PicpArgs& A, const PicpState& s,
+                                               const float* tw, int j, PicpState& ns) {
+  float R[9], t[3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = s.R[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = s.t[i];
+  float chi_prev = s.chi_prev;
+  RoundOut o;
+  finish_round_pose(A, tw, j, R, t, chi_prev, o);
+  store_state(&ns, R, t, chi_prev, o, j);
 }
 
 // Finish round (j-1) of a problem from its block-partial totals (double): H, b, stats -> new

@@ -264,6 +264,36 @@ __device__ __forceinline__ unsigned mm_shift_in_ge0(unsigned m, int v) {
   return m;
 }
 
+// The 16-element candidate mask of one accumulator (bit 15-i = element i >= 0) as ONE asm block:
+// as 16 separate statements the compiler pads every boundary with an s_nop (it cannot see that a
+// VCC carry chain has no hazard), 16 issue slots per taken block.  The caller has already read
+// every accumulator element (the max tree), so the MFMA result hazard is resolved.
+__device__ __forceinline__ unsigned mm_mask16_ge0(const mm_f16v& acc) {
+  unsigned m = 0;
+  asm("v_cmp_le_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %3\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %4\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %5\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %6\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %7\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %8\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %9\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %10\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %11\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %12\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %13\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %14\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %15\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
+      "v_cmp_le_i32 vcc, 0, %16\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+      : "+v"(m)
+      : "v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]), "v"(acc[4]), "v"(acc[5]), "v"(acc[6]),
+        "v"(acc[7]), "v"(acc[8]), "v"(acc[9]), "v"(acc[10]), "v"(acc[11]), "v"(acc[12]), "v"(acc[13]),
+        "v"(acc[14]), "v"(acc[15])
+      : "vcc");
+  return m;
+}
+
 // RAD = 1: the accept-only (radius) form for callers that consume only accepted[] and the
 // best_idx of accepted queries (the VO sequence): pass 1 is skipped and the candidates are the
 // references within a fixed radius of the query (mm_radius below); best_idx, best_dist and
@@ -576,9 +606,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
             if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
               // the candidate mask in two instructions per element (the max tree above has
               // already read every accumulator, so the asm is not the MFMA result's first reader)
-              unsigned m = 0;
-#pragma unroll
-              for (int i = 0; i < 16; ++i) m = mm_shift_in_ge0(m, __float_as_int(acc[i]));
+              unsigned m = mm_mask16_ge0(acc);
               while (m) {
                 const int i = 15 - __builtin_ctz(m);
                 m &= m - 1;
@@ -671,12 +699,38 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       // yields exactly those for ANY visiting order (a tie with the best keeps the smaller
       // index and makes second equal to best; NaN never updates; distances are sums of squares,
       // never -0), so no sort is needed.
-      for (int k = 0; k < n; ++k) {
-        const int j = s_list[w][lane][k];
-        const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
-        if (d < best) { second = best; best = d; bi = j; }
-        else if (d == best) { second = best; bi = min(bi, j); }
-        else if (d < second) second = d;
+      // Candidates in chunks of MM_RQ: every row of a chunk is requested before the first
+      // distance (one L2 round trip per chunk instead of one per candidate; ~2-3 candidates per
+      // query on C5, so usually one chunk).
+      constexpr int MM_RQ = 4;
+      for (int k0 = 0; k0 < n; k0 += MM_RQ) {
+        float rr[MM_RQ][DMAX];
+        int jj[MM_RQ];
+#pragma unroll
+        for (int u = 0; u < MM_RQ; ++u) {
+          jj[u] = (k0 + u < n) ? s_list[w][lane][k0 + u] : -1;
+          const float* rp = r_desc + (P.r_off + max(jj[u], 0)) * dim;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) rr[u][k] = (jj[u] >= 0 && k < dim) ? rp[k] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < MM_RQ; ++u) {
+          if (jj[u] < 0) continue;
+          const int j = jj[u];
+          float d = 0.0f;  // mm_exact_dist over the registers (compile-time indices)
+          {
+#pragma clang fp contract(off)
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k)
+              if (k < dim) {
+                const float t = q[k] - rr[u][k];
+                d = d + t * t;
+              }
+          }
+          if (d < best) { second = best; best = d; bi = j; }
+          else if (d == best) { second = best; bi = min(bi, j); }
+          else if (d < second) second = d;
+        }
       }
     }
     const int64_t o = P.q_off + qi;

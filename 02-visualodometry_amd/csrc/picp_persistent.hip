@@ -63,13 +63,12 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
     unsigned long long* gpart, unsigned long long* gpose, unsigned int* err, unsigned int* tagbase,
     unsigned long long timeout_ticks) {
-  __shared__ double s_red[PICP_PBLOCK / 64][PICP_NPART + 1];
+  __shared__ double s_red[PICP_NPART][PICP_PBLOCK / 64];  // term-major: one row per combining lane
   __shared__ float s_tot[PICP_NPART];
   __shared__ float s_wave[PICP_PBLOCK / 64][PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
   __shared__ int s_tmo;  // a wait of this block timed out (the error word is for the host)
-  __shared__ PicpState s_st;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nblk = A.nblk_u;
@@ -120,7 +119,6 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
     s_done = s.done;
     s_tmo = 0;
-    s_st = s;
     if (leader && s.done) st_out[p] = s;
   }
   __syncthreads();
@@ -135,6 +133,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
   const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
 
+  float chi_prev = FLT_MAX;  // the leader's loop state besides the pose (exec/icp_test.cpp:89)
   for (unsigned epoch = 1; !s_done; ++epoch) {
     // every wait of this round is bounded from the round's start (a whole solve may take far
     // longer than timeout_ticks at large max_rounds; one round never does)
@@ -193,6 +192,8 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       u32x4 gv[MAXG];
       // re-poll only the pairs whose tags have not both matched yet: a full 50 KB sweep costs
       // ~0.5 us at one block's share of the fabric, a re-poll of the few late blocks far less
+      // (a probe-first sweep -- only each block's last pair polled until it arrives -- measured
+      // 17 % slower on C2: the pass is a round trip, not bandwidth, and the probe adds one)
       unsigned pending = 0;
 #pragma unroll
       for (int i = 0; i < MAXG; ++i) {
@@ -231,49 +232,63 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       acc0 += __shfl_xor(acc0, 32);
       acc1 += __shfl_xor(acc1, 32);
       if (lane < 16) {
-        s_red[wave][2 * c] = acc0;
-        s_red[wave][2 * c + 1] = acc1;
+        s_red[2 * c][wave] = acc0;
+        s_red[2 * c + 1][wave] = acc1;
       }
       __syncthreads();
       PSTAMP(2);
       // ---- finish the round in wave 0 only: lanes < 32 combine the groups (fixed order), then
-      //      lanes 0-15 all run the solve (uniform work, one lane's latency) and each publishes
-      //      its pose word directly; the other waves meet wave 0 at the barrier below, off the
-      //      publish path ----
+      //      the wave finishes the round (every lane computes the same values) and
+      //      lanes 0-15 each publish their pose word directly; the other waves meet wave 0 at
+      //      the barrier below, off the publish path ----
       if (wave == 0) {
-        if (lane < PICP_NPART) {
-          double t = 0.0;
+        // the pose: kept from the round start when the linearize leaves registers to spare (one
+        // item per lane), else re-read here (three 16-B LDS loads, landing during the combine):
+        // kept live through a register-bound linearize it spilled; s_pose changes only after the
+        // finish
+        float pr[9], pt[3];
+        if constexpr (NPT == 1) {
+          pr[0] = T.r00; pr[1] = T.r10; pr[2] = T.r20; pr[3] = T.r01; pr[4] = T.r11; pr[5] = T.r21;
+          pr[6] = T.r02; pr[7] = T.r12; pr[8] = T.r22; pt[0] = T.t0; pt[1] = T.t1; pt[2] = T.t2;
+        } else {
 #pragma unroll
-          for (int w = 0; w < PICP_PBLOCK / 64; ++w) t += s_red[w][lane];
+          for (int i = 0; i < 9; ++i) pr[i] = s_pose[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) pt[i] = s_pose[9 + i];
+        }
+        if (lane < PICP_NPART) {
+          double ws[PICP_PBLOCK / 64];  // every load issued before the first add
+#pragma unroll
+          for (int w = 0; w < PICP_PBLOCK / 64; ++w) ws[w] = s_red[lane][w];
+          double t = ws[0];
+#pragma unroll
+          for (int w = 1; w < PICP_PBLOCK / 64; ++w) t += ws[w];
           s_tot[lane] = total_word(A, lane, t);  // lane e converts total e
         }
         __builtin_amdgcn_wave_barrier();
-        if (lane < PICP_POSE_GRAN) {
-          float tw[PICP_NPART];
-#pragma unroll
-          for (int i = 0; i < PICP_NPART; ++i) tw[i] = s_tot[i];
-          PicpState ns;
+        {
+          // the wave finishes the round (every lane the same values, loop state in registers)
+          RoundOut o;
           PSTAMP(4);
-          finish_round_f(A, s_st, tw, (int)epoch, ns);
+          finish_round_pose(A, s_tot, (int)epoch, pr, pt, chi_prev, o);
           PSTAMP(5);
-          if (s_tmo) ns.done = 1;  // a sweep timed out
-          // ---- publish the new pose (and the done flag): lane l owns word l ----
+          if (s_tmo) o.done = 1;  // a sweep timed out
+          // ---- publish the new pose (and the done flag): lane l < 16 owns word l ----
           float w = 0.0f;
 #pragma unroll
-          for (int i = 0; i < 9; ++i) w = (lane == i) ? ns.R[i] : w;
+          for (int i = 0; i < 9; ++i) w = (lane == i) ? pr[i] : w;
 #pragma unroll
-          for (int i = 0; i < 3; ++i) w = (lane == 9 + i) ? ns.t[i] : w;
-          w = (lane == 12) ? __int_as_float(ns.done) : w;
-          __hip_atomic_store(prob_pose + lane, granule(tbase + epoch, w), RLX_AGENT);
+          for (int i = 0; i < 3; ++i) w = (lane == 9 + i) ? pt[i] : w;
+          w = (lane == 12) ? __int_as_float(o.done) : w;
+          if (lane < PICP_POSE_GRAN) __hip_atomic_store(prob_pose + lane, granule(tbase + epoch, w), RLX_AGENT);
           if (lane == 0) {
-            s_st = ns;
 #pragma unroll
-            for (int i = 0; i < 9; ++i) s_pose[i] = ns.R[i];
+            for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) s_pose[9 + i] = ns.t[i];
-            s_done = ns.done;
-            if (ns.done) {
-              st_out[p] = ns;
+        for (int i = 0; i < 3; ++i) s_pose[9 + i] = pt[i];
+            s_done = o.done;
+            if (o.done) {
+              store_state(st_out + p, pr, pt, chi_prev, o, (int)epoch);
               // every block of the problem read tbase before publishing round 1, and this is
               // after its last round: the next launch's tags start past this one's
               __hip_atomic_store(tbase_p, tbase + epoch, RLX_AGENT);

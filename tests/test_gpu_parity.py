@@ -36,6 +36,38 @@ def _synth():
     return synth
 
 
+def _chi_gate(T, K, xyz, uv, rows=480, cols=640):
+    """float64 restatement of the gate of src/picp_solver.cpp:56-91 (projectPoint of
+    src/camera.h:24-36, then chi = |e|^2): (projectable, chi) per correspondence at pose T."""
+    T = np.asarray(T, np.float64)
+    pc = xyz.astype(np.float64) @ T[:3, :3].T + T[:3, 3]
+    z = pc[:, 2]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        pi = pc @ np.asarray(K, np.float64).T
+        u, v = pi[:, 0] / pi[:, 2], pi[:, 1] / pi[:, 2]
+    ok = (z > 0) & (u >= 0) & (u <= cols - 1) & (v >= 0) & (v <= rows - 1)
+    chi = np.where(ok, (u - uv[:, 0]) ** 2 + (v - uv[:, 1]) ** 2, np.inf)
+    return ok, chi
+
+
+def _assert_n_in_explained(K, xyz, uv, T_gpu, T_ref, n_gpu, n_ref, thr=THR):
+    """After a 50-round solve the GPU and oracle poses differ in the last bits, so a point whose
+    chi lies within that difference of the threshold may be gated differently.  Instead of a
+    fixed slack, the difference in n_in must be covered by the points that are ambiguous between
+    the two poses: chi within 4x the largest per-point chi change between them (plus a 1e-6
+    relative floor) of the threshold, or a projectability change."""
+    if n_gpu == n_ref:
+        return
+    ok_g, chi_g = _chi_gate(T_gpu, K, xyz, uv)
+    ok_r, chi_r = _chi_gate(T_ref, K, xyz, uv)
+    both = ok_g & ok_r
+    move = float(np.abs(chi_g[both] - chi_r[both]).max()) if both.any() else 0.0
+    band = 4.0 * move + 1e-6 * thr
+    ambiguous = int((both & (np.abs(chi_r - thr) <= band)).sum() + (ok_g != ok_r).sum())
+    assert abs(n_gpu - n_ref) <= ambiguous, (n_gpu, n_ref, ambiguous, move)
+    assert ambiguous <= max(2, len(xyz) // 1000), (ambiguous, move)  # the band stays narrow
+
+
 def _lin_close(got, ref, rtol=1e-5):
     sH = np.abs(ref["H"]).max()
     np.testing.assert_allclose(got["H"], ref["H"], rtol=rtol, atol=rtol * sH)
@@ -141,7 +173,7 @@ def test_solve_matches_oracle(native, oracle, n, seed, of, keep):
     assert st["rounds"] == 50 and st["ok"] == 1
     assert synth.se3_log_norm(s.pose(), T_ref) < POSE_TOL
     assert synth.se3_log_norm(s.pose(), T_f) < POSE_TOL
-    assert abs(st["n_in"] - st_ref["n_in"]) <= max(2, n // 10000)
+    _assert_n_in_explained(p["K"], p["xyz"], p["uv"], s.pose(), T_ref, st["n_in"], st_ref["n_in"])
     if not keep:  # keep_outliers=True: the saturated outliers still pull (biased, as in the reference)
         assert synth.se3_log_norm(s.pose(), p["T_gt"]) < 1e-2
 
@@ -351,7 +383,7 @@ def test_full_size_c2_c3_properties(native, oracle):
                                          p["u"], p["v"], THR, mode=oracle.MODE_F64, max_rounds=50,
                                          conv_eps=-1.0)
         assert synth.se3_log_norm(T, T_ref) < POSE_TOL
-        assert abs(st["n_in"] - st_ref["n_in"]) <= 10
+        _assert_n_in_explained(p["K"], p["xyz"], p["uv"], T, T_ref, st["n_in"], st_ref["n_in"])
 
 
 def _batch_mode(native, sizes, mode, **kw):
@@ -387,7 +419,7 @@ def test_persistent_and_graph_modes_agree_with_oracle(native, oracle, n, of, kee
                                      conv_eps=conv)
     for mode, (T, st) in res.items():
         assert synth.se3_log_norm(T, T_ref) < _pose_tol(n), mode
-        assert abs(st["n_in"] - st_ref["n_in"]) <= max(2, n // 100000), mode
+        _assert_n_in_explained(p["K"], p["xyz"], p["uv"], T, T_ref, st["n_in"], st_ref["n_in"])
         if conv < 0:
             assert st["rounds"] == 50
     assert res["persistent"][1]["rounds"] == res["graph"][1]["rounds"]

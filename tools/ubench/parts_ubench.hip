@@ -1,0 +1,79 @@
+// Microbenchmark (diagnostic, not shipped): cycles of the pieces of finish_round_f on one wave.
+#include <cstdio>
+#include <vector>
+#include "picp_device.h"
+using namespace picp;
+
+// MODE 0: finish_round_pose (tw in LDS, loop state in registers), 1: ldl6_solve (tw in LDS),
+//      2: apply_update (registers), 3: LDS state copy (s_st -> ns -> s_st), 4: empty loop
+template <int MODE>
+__global__ void bench(PicpArgs A, const float* tot0, int iters, unsigned long long* cyc, float* out) {
+  __shared__ float s_tot[PICP_NPART];
+  __shared__ PicpState s_st;
+  const int lane = threadIdx.x;
+  if (lane < PICP_NPART) s_tot[lane] = tot0[lane];
+  if (lane == 0) {
+    PicpState s{};
+    for (int i = 0; i < 9; ++i) s.R[i] = (i % 4 == 0) ? 1.0f : 0.0f;
+    s_st = s;
+  }
+  __syncthreads();
+  float R[9], t[3] = {0, 0, 0}, dx[6] = {1e-4f, 2e-4f, 3e-4f, 1e-5f, 2e-5f, 3e-5f};
+  for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : 0.0f;
+  float acc = 0.0f, chi_prev = 1e30f;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    if (MODE == 0) {  // the whole finish as the kernels run it (pose + chi_prev in registers)
+      RoundOut o;
+      finish_round_pose(A, s_tot, it + 1, R, t, chi_prev, o);
+      if (lane == 0) s_tot[PICP_P_B] = tot0[PICP_P_B] + R[1] * 1e-30f;  // loop-carried
+    } else if (MODE == 1) {
+      ldl6_solve(s_tot, dx);
+      if (lane == 0) s_tot[PICP_P_B] = tot0[PICP_P_B] + dx[5] * 1e-30f;
+    } else if (MODE == 2) {
+      apply_update(dx, R, t);
+      dx[3] = R[1] * 1e-3f;
+    } else if (MODE == 3) {
+      PicpState ns;
+      const PicpState& s = s_st;
+      for (int i = 0; i < 9; ++i) ns.R[i] = s.R[i];
+      for (int i = 0; i < 3; ++i) ns.t[i] = s.t[i];
+      ns.chi_prev = s.chi_prev; ns.done = s.done; ns.ok = s.ok; ns.converged = s.converged;
+      for (int i = 0; i < 11; ++i) ns.pad[i] = 0;
+      ns.chi_in = s_tot[27]; ns.chi_out = s_tot[28]; ns.n_in = it; ns.n_proj = it; ns.rounds = it;
+      ns.R[0] += 1e-30f;
+      if (lane == 0) s_st = ns;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  acc = dx[0] + dx[5] + R[0] + t[0] + s_st.R[0];
+  if (lane == 0) { cyc[MODE] = (t1 - t0) / iters; out[MODE] = acc; }
+}
+
+int main() {
+  PicpArgs A{};
+  A.damping = 1.0f; A.min_inliers = 0; A.max_rounds = 1 << 30; A.conv_eps = -1.0f;
+  std::vector<float> tot(PICP_NPART, 0.0f);
+  int k = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c) tot[k++] = (r == c) ? 1e4f + 100.0f * r : 10.0f * (r + c + 1);
+  for (int i = 0; i < 6; ++i) tot[PICP_P_B + i] = 1e-3f * (i + 1);
+  float* d_tot; unsigned long long* d_cyc; float* d_out;
+  hipMalloc(&d_tot, PICP_NPART * 4); hipMalloc(&d_cyc, 8 * 8); hipMalloc(&d_out, 8 * 4);
+  hipMemcpy(d_tot, tot.data(), PICP_NPART * 4, hipMemcpyHostToDevice);
+  const int iters = 2000;
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(bench<0>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipLaunchKernelGGL(bench<1>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipLaunchKernelGGL(bench<2>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipLaunchKernelGGL(bench<3>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipLaunchKernelGGL(bench<4>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipDeviceSynchronize();
+  }
+  unsigned long long cyc[8];
+  hipMemcpy(cyc, d_cyc, 64, hipMemcpyDeviceToHost);
+  printf("cycles/iter: finish_round_pose %llu  ldl6_solve %llu  apply_update %llu  state_copy %llu  empty %llu\n",
+         cyc[0], cyc[1], cyc[2], cyc[3], cyc[4]);
+  return 0;
+}
