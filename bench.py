@@ -80,13 +80,21 @@ def launch_ranks(n):
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     rc = 0
     try:
-        for p in procs:
-            p.wait()
-            if p.returncode != 0 and rc == 0:
-                rc = p.returncode
-                for q in procs:  # one rank failed: the others would block in a collective
+        # poll every rank (not in rank order): a rank that fails leaves the others blocked in a
+        # collective, so the first failure anywhere terminates the rest
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                for q in procs:
                     if q.poll() is None:
                         q.terminate()
+                break
+            time.sleep(0.1)
+        for p in procs:
+            p.wait()
+            if rc == 0 and p.returncode != 0:
+                rc = p.returncode
     finally:
         for q in procs:
             if q.poll() is None:
@@ -570,6 +578,8 @@ def plan_only(args, rk):
     from picp_amd.dist import shard_range
     total = args.problems or WORKLOADS["c4"]["problems"]
     n = args.n or 256
+    if os.environ.get("PICP_PLAN_FAIL_RANK") == str(rk.rank):  # launcher test: one rank dies
+        sys.exit(3)
     f0, f1 = shard_range(total, rk.world, rk.rank)
     bt = synth.make_batch(f1 - f0, n, base_seed=1000, first=f0)
     from picp_amd.vo_synth import segments

@@ -106,3 +106,21 @@ def test_bench_launcher_gpus2_plan_only_starts_shards_and_gathers():
         f0, f1 = x["c4_frames"]
         bt = synth.make_batch(f1 - f0, 64, base_seed=1000, first=f0)
         assert x["c4_checksum"] == float(np.float64(bt["xyz"]).sum() + np.float64(bt["uv"]).sum())
+
+
+def test_bench_launcher_one_failing_rank_ends_the_job():
+    """A rank that dies (here rank 1, before the gather its peer blocks in) must end the whole
+    launch with a failure, not leave rank 0 waiting in a collective forever (rank 0 may see the
+    broken connection and fail first: either exit code is a failure)."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PICP_PLAN_FAIL_RANK"] = "1"
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plan-only",
+                        "--problems", "9", "--n", "64", "--frames", "200"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0, (r.returncode, r.stderr[-2000:])
+    assert time.time() - t0 < 200
