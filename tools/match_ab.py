@@ -16,6 +16,13 @@ rng = np.random.default_rng(0)
 P, nq, nr = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 variants = (sys.argv[4] if len(sys.argv) > 4 else "PICP_MATCH_ACCEPT_ONLY=0;PICP_MATCH_ACCEPT_ONLY=1").split(";")
 d2s = [rng.uniform(-1, 1, (nr, 10)).astype(np.float32) for _ in range(P)]
+# MATCH_DUP=f: the last f*nr references re-use earlier rows (+1e-3 noise), as duplicated map
+# landmarks do in the VO sequence (C5: ~2.2 candidates per query)
+dup = float(os.environ.get("MATCH_DUP", "0"))
+if dup > 0:
+    k = int(dup * nr)
+    for d2 in d2s:
+        d2[nr - k:] = d2[:k] + rng.normal(0, 1e-3, (k, 10)).astype(np.float32)
 d1s = []
 for d2 in d2s:
     d1 = rng.uniform(-1, 1, (nq, 10)).astype(np.float32)
