@@ -603,9 +603,19 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
             int mx = __float_as_int(acc[0]);
 #pragma unroll
             for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
+#ifdef MM_DIAG_NOVOTE  // diagnostic timing build only: MFMA + max tree, no vote, no candidates
+            if (mx == 0x7fffffff) c_n = 0;
+            if (false) {
+#elif defined(MM_DIAG_NOCAND)  // diagnostic timing build only: vote, no candidate extraction
+            if (__any(mx >= 0)) c_n = 0;
+            if (false) {
+#else
             if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
+#endif
               // the candidate mask in two instructions per element (the max tree above has
-              // already read every accumulator, so the asm is not the MFMA result's first reader)
+              // already read every accumulator, so the asm is not the MFMA result's first reader);
+              // a wave vote per element instead (skip the elements no lane has a candidate in)
+              // measured 1.6x slower: 16 uniform branches, and 140 VGPRs cost a wave per SIMD
               unsigned m = mm_mask16_ge0(acc);
               while (m) {
                 const int i = 15 - __builtin_ctz(m);
@@ -679,7 +689,11 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     for (int k = 0; k < DMAX; ++k) q[k] = (k < dim) ? q_desc[(P.q_off + qi) * dim + k] : 0.0f;
     float best = FLT_MAX, second = FLT_MAX;  // :78-79
     int32_t bi = -1;
+#ifdef MM_DIAG_NORESCAN  // diagnostic timing build only: no exact rescan
+    const int n = 0;
+#else
     const int n = s_cnt[w][lane];
+#endif
 #ifdef PICP_STAMPS
     atomicAdd(&picp_match_stats[2], 1ull);
     atomicAdd(&picp_match_stats[1], (unsigned long long)n);

@@ -1,7 +1,10 @@
 #!/bin/bash
 # matcher time decomposition: kernel traces of one accept-only 1024 x 2000 x 2000 batch (half of
 # the queries with an exact match, half the references duplicated) for the shipped build and the
-# diagnostic timing builds (no candidate extraction / no rescan / no vote: wrong results, timing only)
+# diagnostic timing builds (no candidate extraction / no rescan / no vote: wrong results, timing only).
+# Build them first, in 02-visualodometry_amd/, per variant V in NOCAND NORESCAN "NOCAND -DMM_DIAG_NORESCAN"
+# "NOVOTE -DMM_DIAG_NORESCAN": hipcc ... -DMM_DIAG_$V -c csrc/picp_match.hip, then link it with the other
+# build/*.o objects into lib/libpicp_amd_d_<v>.so (the Makefile's $(LIB) rule with that object).
 export TMPDIR=/tmp
 OUT=gpurun_out/mdiag
 mkdir -p $OUT
