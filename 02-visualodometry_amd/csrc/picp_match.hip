@@ -551,20 +551,18 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   }  // pass 1
 
   // ---------------- pass 2: collect the candidates ----------------
-  // Candidates are buffered per lane in registers and appended to the LDS lists after the pass
-  // (no LDS atomic round trip inside the MFMA loop); a lane whose buffer is full flushes it early
-  // (rare: 2.2 candidates per query on C5, tools/match_stats.py).
-  constexpr int MM_LB = 4;
-  int c_row[MM_LB], c_ref[MM_LB];
+  // Each lane appends its candidates (row, reference) to its OWN list in LDS -- this wave's
+  // s_list words viewed as [64 lanes][LCAP] -- with one plain store each: no atomic and no
+  // register-indexed buffer inside the MFMA loop.  After the pass the wave scatters the entries
+  // into the per-query lists the rescan reads (~2.2 candidates per query on C5, so a lane holds a
+  // few; one that overflows sends every query of its wave to the full scan).  Entries pack the
+  // row (< 64) above a reference index < 2^26 (larger sets take the full scan).
+  constexpr int LCAP = QPW * MM_CAP / 64;  // RB = 2: 16, RB = 1: 8
+  int* const lane_list = &s_list[w][0][0] + lane * LCAP;
   int c_n = 0;
-  auto flush = [&]() {
-#pragma unroll
-    for (int k = 0; k < MM_LB; ++k)
-      if (k < c_n) {
-        const int slot = atomicAdd(&s_cnt[w][c_row[k]], 1);
-        if (slot < MM_CAP) s_list[w][c_row[k]][slot] = c_ref[k];
-      }
-    c_n = 0;
+  auto push = [&](int row, int ref) {
+    if (c_n < LCAP) lane_list[c_n] = (int)(((unsigned)row << 26) | (unsigned)ref);
+    ++c_n;
   };
   fetch(0);
   if constexpr (RAD == 2) my_nofold = fold_check(0);
@@ -620,15 +618,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
               while (m) {
                 const int i = 15 - __builtin_ctz(m);
                 m &= m - 1;
-                if (c_n == MM_LB) flush();
-                const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
-#pragma unroll
-                for (int k = 0; k < MM_LB; ++k)
-                  if (k == c_n) {
-                    c_row[k] = row;
-                    c_ref[k] = (int)(t0 + col);
-                  }
-                ++c_n;
+                push(32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf, (int)(t0 + col));
               }
             }
           }
@@ -660,15 +650,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         while (m) {  // rare: the few candidates of this lane's 16 rows (bit 15-i = element i)
           const int i = 15 - __builtin_ctz(m);
           m &= m - 1;
-          if (c_n == MM_LB) flush();
-          const int row = 32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf;
-#pragma unroll
-          for (int k = 0; k < MM_LB; ++k)  // register-indexed append (no scratch)
-            if (k == c_n) {
-              c_row[k] = row;
-              c_ref[k] = (int)(t0 + col);
-            }
-          ++c_n;
+          push(32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf, (int)(t0 + col));
         }
       }
     }
@@ -677,8 +659,26 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       stash(buf ^ 1);
     }
   }
-  __syncthreads();
-  flush();
+  // scatter the lane lists into the per-query lists (the same LDS words): every entry of the wave
+  // is read into registers and the reads have completed before the first write
+  {
+    const int ln = min(c_n, LCAP);
+    unsigned ent[LCAP];
+#pragma unroll
+    for (int u = 0; u < LCAP; ++u) ent[u] = (u < ln) ? (unsigned)lane_list[u] : 0u;
+    const bool ovf = __any(c_n > LCAP) || P.nr >= ((int64_t)1 << 26);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < LCAP; ++u)
+      if (u < ln) {
+        const int row = (int)(ent[u] >> 26);
+        const int slot = atomicAdd(&s_cnt[w][row], 1);
+        if (slot < MM_CAP) s_list[w][row][slot] = (int)(ent[u] & 0x3ffffffu);
+      }
+    // a dropped entry (full lane list) or a reference index past the packing: the full scan
+    if (ovf && lane < QPW) s_cnt[w][lane] = MM_CAP + 1;
+  }
   __syncthreads();
 
   // ---------------- exact update over the candidates, in index order ----------------
