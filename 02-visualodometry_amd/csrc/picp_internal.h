@@ -110,7 +110,8 @@ struct VoStep {     // per pose slot; slot 0 of a segment = the bootstrap
 struct VoArgs {     // by value; every pointer is device memory
   float K[9];
   int32_t dim;
-  int32_t n_seg;
+  int32_t n_seg;             // segments of this launch: seg0 .. seg0 + n_seg - 1
+  int32_t seg0;
   const int64_t* frame_off;  // n_frames + 1
   const float2* uv;          // per observation
   const float* desc;         // per observation, dim floats

@@ -97,7 +97,7 @@ __device__ inline int vo_block_rank(bool flag, int* s_cnt, int* total) {
 }
 
 __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int t) {
-  const int s = blockIdx.x;
+  const int s = a.seg0 + (int)blockIdx.x;
   const VoSegment G = a.segs[s];
   const int64_t base = (int64_t)s * a.cap_c;
   __shared__ int s_cnt[VO_WAVES];
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
 }
 
 __global__ __launch_bounds__(VOA_BLOCK) void vo_append_kernel(const VoArgs a, int t) {
-  const int s = blockIdx.x;
+  const int s = a.seg0 + (int)blockIdx.x;
   const VoSegment G = a.segs[s];
   const bool boot = t < 0;
   if (!boot && t >= G.steps) return;

@@ -75,7 +75,27 @@ struct picp_vo {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool use_graph = true;
+  // The sequence is enqueued launch by launch (PICP_VO_GRAPH=1: captured once into a hipGraph
+  // and replayed).  With the step chains and the side stream on prioritised streams the direct
+  // enqueue measured faster than the graph, whose replay does not keep the streams' priorities
+  // or the chains' phase offset.
+  bool use_graph = false;
+  // the frame->next match in chunks by step index (chunk k = frame f0+k of every segment with
+  // more than k steps), chunks 1.. on a side stream that runs beside the step chain
+  std::vector<size_t> chunk_off;  // pprobs[chunk_off[k] .. chunk_off[k+1]) is chunk k
+  bool overlap = true;            // PICP_VO_OVERLAP=0: every chunk on the main stream, up front
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr;
+  std::vector<hipEvent_t> ev_chunk;
+  // the segments in `chains` contiguous groups, each group's step chain on its own stream
+  // (group 0 on the handle's stream): one group's latency-bound PICP block kernel runs beside
+  // another group's throughput-bound world match.  Group c starts after group c-1's first world
+  // match (PICP_VO_PHASE=0: together), so the groups run out of phase.
+  int chains = 2;  // PICP_VO_CHAINS
+  bool phase = true;
+  std::vector<hipStream_t> cstream;  // [chains], [0] unused (the handle's stream)
+  std::vector<hipEvent_t> ev_cj;     // [chains]: group c's end (join), [0]: fork
+  std::vector<hipEvent_t> ev_ph;     // [chains]: group c's first world match done
   int accept_only = 1;  // the sequence reads only accepted matches (PICP_VO_MATCH_FULL=1: full form)
 };
 
@@ -84,6 +104,9 @@ static void vo_free_segments(picp_vo* h) {
   if (h->graph) hipGraphDestroy(h->graph);
   h->exec = nullptr;
   h->graph = nullptr;
+  for (hipEvent_t e : h->ev_chunk)
+    if (e) hipEventDestroy(e);
+  h->ev_chunk.clear();
   if (h->seg_mem) hipFree(h->seg_mem);
   h->seg_mem = nullptr;
   h->n_seg = 0;
@@ -99,6 +122,14 @@ extern "C" int picp_vo_destroy(picp_vo_t* h) {
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->side) hipStreamDestroy(h->side);
+  for (hipEvent_t e : h->ev_cj)
+    if (e) hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_ph)
+    if (e) hipEventDestroy(e);
+  for (hipStream_t c : h->cstream)
+    if (c) hipStreamDestroy(c);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return PICP_OK;
@@ -137,6 +168,12 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   h->frame_off.assign(frame_off, frame_off + n_frames + 1);
   if (const char* e = getenv("PICP_VO_GRAPH")) h->use_graph = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_MATCH_FULL")) h->accept_only = atoi(e) != 0 ? 0 : 1;
+  if (const char* e = getenv("PICP_VO_OVERLAP")) h->overlap = atoi(e) != 0;
+  // at most two groups: three or more gave poses that were not bit-identical to one group on
+  // MI355X (ROCm 7.2), with every group's ordering intact on paper; two were identical in every
+  // repetition (tools/vo_chains_check.py)
+  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
+  if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
   do {                            \
@@ -151,9 +188,25 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
     return PICP_OK;
   };
   VO_TRY([&]() -> int {
-    HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    // the step chains' streams at the highest priority, the side stream at the lowest
+    // (PICP_VO_PRIO=0: all at the default)
+    int lo = 0;
+    int hi = 0;
+    const char* pe = getenv("PICP_VO_PRIO");
+    if (!(pe && atoi(pe) == 0)) HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
+    HIP_TRY(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, lo));
     HIP_TRY(hipEventCreate(&h->ev0));
     HIP_TRY(hipEventCreate(&h->ev1));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    h->cstream.assign((size_t)h->chains, nullptr);
+    h->ev_cj.assign((size_t)h->chains, nullptr);
+    h->ev_ph.assign((size_t)h->chains, nullptr);
+    for (int c = 0; c < h->chains; ++c) {
+      if (c > 0) HIP_TRY(hipStreamCreateWithPriority(&h->cstream[c], hipStreamNonBlocking, hi));
+      HIP_TRY(hipEventCreateWithFlags(&h->ev_cj[c], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&h->ev_ph[c], hipEventDisableTiming));
+    }
     return PICP_OK;
   }());
   VO_TRY(alloc((void**)&h->frame_off_d, (size_t)(n_frames + 1) * sizeof(int64_t)));
@@ -219,10 +272,22 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     max_steps = std::max(max_steps, (int)G.steps);
     for (int64_t f = G.f0; f < G.f0 + G.steps; ++f) is_curr[f] = 1;
   }
+  // frame->next problems grouped by step index: chunk k holds frame f0+k of every segment with
+  // more than k steps (the bootstrap and step 0 read chunk 0, step t reads chunk t).  Frames of
+  // overlapping segments are matched once, in the first chunk that needs them.
   std::vector<MatchProblem> pprobs;
-  for (int64_t f = 0; f + 1 < h->n_frames; ++f)
-    if (is_curr[f] && frame_n(h, f) > 0)
-      pprobs.push_back(MatchProblem{h->frame_off[f], frame_n(h, f), h->frame_off[f + 1], frame_n(h, f + 1)});
+  std::vector<size_t> chunk_off(1, 0);
+  std::vector<char> done((size_t)h->n_frames, 0);
+  for (int k = 0; k < max_steps; ++k) {
+    for (int s = 0; s < n_seg; ++s) {
+      const int64_t f = first[s] + k;
+      if (k < steps[s] && !done[f] && frame_n(h, f) > 0) {
+        done[f] = 1;
+        pprobs.push_back(MatchProblem{h->frame_off[f], frame_n(h, f), h->frame_off[f + 1], frame_n(h, f + 1)});
+      }
+    }
+    chunk_off.push_back(pprobs.size());
+  }
   int64_t cap_c = (std::max<int64_t>(h->max_obs, 1) + 3) / 4 * 4;
   // register-resident items per lane of picp_block_kernel: the largest power of two whose
   // 512 * npt slots the biggest frame fills (masked slots cost as much as live ones every
@@ -253,6 +318,9 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_mn2 = part((size_t)map_slots * sizeof(float));
   HIP_TRY(hipMalloc(&h->seg_mem, total));
   char* m = (char*)h->seg_mem;
+  h->ev_chunk.assign((size_t)max_steps, nullptr);
+  for (auto& e : h->ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  h->chunk_off = chunk_off;
   h->segs = segs;
   h->pprobs = pprobs;
   h->n_seg = n_seg;
@@ -287,6 +355,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   memcpy(V.K, h->K, sizeof(V.K));
   V.dim = h->dim;
   V.n_seg = n_seg;
+  V.seg0 = 0;
   V.frame_off = h->frame_off_d;
   V.uv = h->uv_d;
   V.desc = h->desc_d;
@@ -326,27 +395,62 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   return PICP_OK;
 }
 
-// the whole sequence, back to back on the handle's stream
-static hipError_t vo_enqueue(picp_vo* h) {
+// frame->next match problems [p0, p1) on stream st, in launches of at most VO_MAX_GRID_Y problems
+static hipError_t vo_frame_match(picp_vo* h, hipStream_t st, size_t p0, size_t p1) {
   hipError_t e = hipSuccess;
-  for (size_t p0 = 0; p0 < h->pprobs.size() && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
-    const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, h->pprobs.size() - p0);
-    e = picp_launch_match_mfma(h->stream, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1,
-                               h->obs_h, h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST,
-                               VO_MATCH_RATIO, h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only);
+  for (; p0 < p1 && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
+    const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - p0);
+    e = picp_launch_match_mfma(st, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1, h->obs_h,
+                               h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
+                               h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only);
+  }
+  return e;
+}
+
+// the whole sequence on the handle's stream.  With overlap on, the frame->next match chunks
+// 1.. run on the side stream (forked after chunk 0, joined by each step's append, which waits
+// for its own chunk): the step chain is a string of latency-bound one-block-per-segment
+// kernels, and the throughput-bound match chunks fill the CUs it leaves idle.
+static hipError_t vo_enqueue(picp_vo* h) {
+  const size_t nck = h->chunk_off.size() - 1;
+  const bool ov = h->overlap && nck > 1;
+  hipError_t e = vo_frame_match(h, h->stream, 0, ov ? h->chunk_off[1] : h->chunk_off[nck]);
+  if (e == hipSuccess && ov) {
+    e = hipEventRecord(h->ev_fork, h->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->side, h->ev_fork, 0);
+    for (size_t k = 1; k < nck && e == hipSuccess; ++k) {
+      e = vo_frame_match(h, h->side, h->chunk_off[k], h->chunk_off[k + 1]);
+      if (e == hipSuccess) e = hipEventRecord(h->ev_chunk[k], h->side);
+    }
   }
   if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
-  const VoArgs& V = h->vargs;
-  for (int t = 0; t < h->max_steps && e == hipSuccess; ++t) {
-    e = picp_launch_match_mfma(h->stream, h->n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
-                               V.map_h, V.map_n1, V.map_n2, h->wprobs_d, h->dim, VO_MATCH_DIST,
-                               VO_MATCH_RATIO, h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
-    if (e == hipSuccess) e = picp_launch_vo_gather(h->stream, &V, t);
-    if (e == hipSuccess)
-      e = picp_launch_block(h->stream, h->n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs,
-                            V.st_in, (PicpState*)V.st_out, (int)h->max_obs, 1, nullptr, nullptr, nullptr, 0);
-    if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &V, t);
+  const int C = std::min(h->chains, h->n_seg);
+  if (e == hipSuccess && C > 1) e = hipEventRecord(h->ev_cj[0], h->stream);  // fork
+  for (int c = 0; c < C && e == hipSuccess; ++c) {
+    hipStream_t st = (c == 0) ? h->stream : h->cstream[c];
+    const int s0 = (int)((int64_t)h->n_seg * c / C), s1 = (int)((int64_t)h->n_seg * (c + 1) / C);
+    VoArgs V = h->vargs;
+    V.seg0 = s0;
+    V.n_seg = s1 - s0;
+    int steps = 0;
+    for (int s = s0; s < s1; ++s) steps = std::max(steps, (int)h->segs[s].steps);
+    if (c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
+    for (int t = 0; t < steps && e == hipSuccess; ++t) {
+      e = picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
+                                 V.map_n1, V.map_n2, h->wprobs_d + s0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
+                                 h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
+      if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
+      if (e == hipSuccess) e = picp_launch_vo_gather(st, &V, t);
+      if (e == hipSuccess)
+        e = picp_launch_block(st, V.n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs + s0,
+                              V.st_in + s0, (PicpState*)V.st_out + s0, (int)h->max_obs, 1, nullptr, nullptr,
+                              nullptr, 0);
+      if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
+      if (e == hipSuccess) e = picp_launch_vo_append(st, &V, t);
+    }
+    if (e == hipSuccess && c > 0) e = hipEventRecord(h->ev_cj[c], st);
   }
+  for (int c = 1; c < C && e == hipSuccess; ++c) e = hipStreamWaitEvent(h->stream, h->ev_cj[c], 0);  // join
   return e;
 }
 

@@ -156,6 +156,43 @@ def test_vo_replay_and_segment_independence(native):
     np.testing.assert_array_equal(seq.map(0)[1], m1[1])
 
 
+@pytest.mark.parametrize("env", [
+    {"PICP_VO_CHAINS": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_PRIO": "0"},  # one stream, in order
+    {"PICP_VO_GRAPH": "1"},  # the graph-captured form of the default schedule
+])
+def test_vo_schedule_invariance(native, monkeypatch, env):
+    """The default schedule (frame->next match chunks on a side stream, the segments in two
+    groups on their own streams, picp_vo_runtime.cpp vo_enqueue) gives poses, step records and
+    maps bit-identical to the serial one-stream order and to its graph replay."""
+    from picp_amd.vo_synth import VOSequence, segments
+    s = VOSequence(1201, obs_per_frame=1200, seed=5)
+    F = s.frames(0, 1201)
+    first, steps = segments(1201, 40)
+    boot = np.stack([[F["T_cw"][f], F["T_cw"][f + 1]] for f in first])
+
+    def run():
+        seq = native.VOSequence(F["frame_off"], F["uv"], F["desc"], K=s.K)
+        seq.set_segments(first, steps, boot)
+        seq.run()
+        seq.run()  # a second run (and, with the graph, a replay) over the same buffers
+        out = (seq.poses(), seq.step_records(), [seq.map(k) for k in (0, len(first) // 2, len(first) - 1)])
+        seq.close()
+        return out
+
+    base = run()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    other = run()
+    for x, y in zip(base[0], other[0]):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(base[1], other[1]):
+        for f in ("n_corr", "n_in", "rounds", "n_new"):
+            np.testing.assert_array_equal(x[f], y[f])
+    for (xa, da), (xb, db) in zip(base[2], other[2]):
+        np.testing.assert_array_equal(xa, xb)
+        np.testing.assert_array_equal(da, db)
+
+
 def test_vo_argument_errors(native):
     from picp_amd.vo_synth import VOSequence
     s = VOSequence(6, obs_per_frame=200, seed=1)
