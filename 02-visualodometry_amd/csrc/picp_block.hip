@@ -63,6 +63,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
     unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks) {
+  PICP_KFENCE_IN();
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   // wave sums, term-major: the lane combining term e reads its BS/64 wave sums as 16-B loads
   __shared__ __attribute__((aligned(16))) float s_wave[PICP_NPART][BS / 64];
@@ -288,6 +289,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
   if (split > 1 && tid == 0) tagbase[blockIdx.x] = tbase + (unsigned)last_round;
   if (h == 0 && tid < 32)
     reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
+  PICP_KFENCE_OUT();
 }
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part (BS 512)

@@ -71,6 +71,21 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 // ---------------------------------------------------------------------------------------
 // descriptor matching (picp_match.hip): query rows [q_off, q_off + nq) of the query
 // descriptors against reference rows [r_off, r_off + nr); best_idx is relative to r_off.
+// Diagnostic build only (-DPICP_KFENCE): explicit agent-scope acquire at the start and release at
+// the end of the VO path's kernels, to test whether kernel-boundary visibility is what differs
+// between schedules.
+#ifdef PICP_KFENCE
+#define PICP_KFENCE_IN() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#define PICP_KFENCE_OUT() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
+#else
+#define PICP_KFENCE_IN() \
+  do {                   \
+  } while (0)
+#define PICP_KFENCE_OUT() \
+  do {                    \
+  } while (0)
+#endif
+
 struct MatchProblem {
   int64_t q_off, nq, r_off, nr;
 };

@@ -316,6 +316,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
     float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
     int xcd_map) {
+  PICP_KFENCE_IN();
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
@@ -753,6 +754,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     second_dist[o] = second;
     accepted[o] = (bi != -1 && best < dist_thr && best / second < ratio_thr) ? 1 : 0;  // :100-103
   }
+  PICP_KFENCE_OUT();
 }
 
 extern "C" int picp_match_prep_kch(int dim) { return dim <= 16 ? 1 : 2; }

@@ -75,15 +75,16 @@ struct picp_vo {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // The sequence is enqueued launch by launch (PICP_VO_GRAPH=1: captured once into a hipGraph
-  // and replayed).  With the step chains and the side stream on prioritised streams the direct
-  // enqueue measured faster than the graph, whose replay does not keep the streams' priorities
-  // or the chains' phase offset.
-  bool use_graph = false;
+  // The sequence is captured once into a hipGraph and replayed (PICP_VO_GRAPH=0: enqueued launch
+  // by launch).  With the concurrent schedule (PICP_VO_OVERLAP=1, PICP_VO_CHAINS=2) the direct
+  // enqueue measured faster: the graph's replay keeps neither the streams' priorities nor the
+  // chains' phase offset.
+  bool use_graph = true;
+  bool graph_env = false;
   // the frame->next match in chunks by step index (chunk k = frame f0+k of every segment with
   // more than k steps), chunks 1.. on a side stream that runs beside the step chain
   std::vector<size_t> chunk_off;  // pprobs[chunk_off[k] .. chunk_off[k+1]) is chunk k
-  bool overlap = true;            // PICP_VO_OVERLAP=0: every chunk on the main stream, up front
+  bool overlap = false;           // PICP_VO_OVERLAP=1 (default off: every chunk on the main stream, up front)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_chunk;
@@ -91,7 +92,7 @@ struct picp_vo {
   // (group 0 on the handle's stream): one group's latency-bound PICP block kernel runs beside
   // another group's throughput-bound world match.  Group c starts after group c-1's first world
   // match (PICP_VO_PHASE=0: together), so the groups run out of phase.
-  int chains = 2;  // PICP_VO_CHAINS
+  int chains = 1;  // PICP_VO_CHAINS (default 1: the serial order)
   bool phase = true;
   std::vector<hipStream_t> cstream;  // [chains], [0] unused (the handle's stream)
   std::vector<hipEvent_t> ev_cj;     // [chains]: group c's end (join), [0]: fork
@@ -166,7 +167,10 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   h->n_obs = n_obs;
   h->max_obs = mx;
   h->frame_off.assign(frame_off, frame_off + n_frames + 1);
-  if (const char* e = getenv("PICP_VO_GRAPH")) h->use_graph = atoi(e) != 0;
+  if (const char* e = getenv("PICP_VO_GRAPH")) {
+    h->use_graph = atoi(e) != 0;
+    h->graph_env = true;
+  }
   if (const char* e = getenv("PICP_VO_MATCH_FULL")) h->accept_only = atoi(e) != 0 ? 0 : 1;
   if (const char* e = getenv("PICP_VO_OVERLAP")) h->overlap = atoi(e) != 0;
   // at most two groups: three or more gave poses that were not bit-identical to one group on
@@ -174,6 +178,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   // repetition (tools/vo_chains_check.py)
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
+  if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
   do {                            \
@@ -195,7 +200,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
     const char* pe = getenv("PICP_VO_PRIO");
     if (!(pe && atoi(pe) == 0)) HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_TRY(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
-    HIP_TRY(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, lo));
+    if (h->overlap) HIP_TRY(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, lo));
     HIP_TRY(hipEventCreate(&h->ev0));
     HIP_TRY(hipEventCreate(&h->ev1));
     HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -317,6 +322,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_mn1 = part((size_t)map_slots * sizeof(float));
   const Part p_mn2 = part((size_t)map_slots * sizeof(float));
   HIP_TRY(hipMalloc(&h->seg_mem, total));
+  HIP_TRY(hipMemset(h->seg_mem, 0, total));  // every table defined before the first run
   char* m = (char*)h->seg_mem;
   h->ev_chunk.assign((size_t)max_steps, nullptr);
   for (auto& e : h->ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -412,6 +418,12 @@ static hipError_t vo_frame_match(picp_vo* h, hipStream_t st, size_t p0, size_t p
 // for its own chunk): the step chain is a string of latency-bound one-block-per-segment
 // kernels, and the throughput-bound match chunks fill the CUs it leaves idle.
 static hipError_t vo_enqueue(picp_vo* h) {
+  // diagnostic only (wrong results): PICP_VO_DIAG_SKIP bit 1 gather, 2 append, 4 PICP, 8 world
+  // match launches left out of the sequence
+  static const int skip = [] {
+    const char* e = getenv("PICP_VO_DIAG_SKIP");
+    return e ? atoi(e) : 0;
+  }();
   const size_t nck = h->chunk_off.size() - 1;
   const bool ov = h->overlap && nck > 1;
   hipError_t e = vo_frame_match(h, h->stream, 0, ov ? h->chunk_off[1] : h->chunk_off[nck]);
@@ -423,7 +435,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
       if (e == hipSuccess) e = hipEventRecord(h->ev_chunk[k], h->side);
     }
   }
-  if (e == hipSuccess) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
+  if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const int C = std::min(h->chains, h->n_seg);
   if (e == hipSuccess && C > 1) e = hipEventRecord(h->ev_cj[0], h->stream);  // fork
   for (int c = 0; c < C && e == hipSuccess; ++c) {
@@ -436,17 +448,18 @@ static hipError_t vo_enqueue(picp_vo* h) {
     for (int s = s0; s < s1; ++s) steps = std::max(steps, (int)h->segs[s].steps);
     if (c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
     for (int t = 0; t < steps && e == hipSuccess; ++t) {
+      if (!(skip & 8))
       e = picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
                                  V.map_n1, V.map_n2, h->wprobs_d + s0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
                                  h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
-      if (e == hipSuccess) e = picp_launch_vo_gather(st, &V, t);
-      if (e == hipSuccess)
+      if (e == hipSuccess && !(skip & 1)) e = picp_launch_vo_gather(st, &V, t);
+      if (e == hipSuccess && !(skip & 4))
         e = picp_launch_block(st, V.n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs + s0,
                               V.st_in + s0, (PicpState*)V.st_out + s0, (int)h->max_obs, 1, nullptr, nullptr,
                               nullptr, 0);
       if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
-      if (e == hipSuccess) e = picp_launch_vo_append(st, &V, t);
+      if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
     }
     if (e == hipSuccess && c > 0) e = hipEventRecord(h->ev_cj[c], st);
   }
@@ -539,6 +552,15 @@ extern "C" int picp_vo_get_map(picp_vo_t* h, int seg, int64_t cap, float* xyz, f
   if (desc && k)
     HIP_TRY(hipMemcpy(desc, h->vargs.map_desc + off * h->dim, (size_t)k * h->dim * sizeof(float),
                       hipMemcpyDeviceToHost));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_debug_matches(picp_vo_t* h, int which, int32_t* dst) {
+  CHECK_ARG(h && dst && which >= 0 && which <= 3, "picp_vo_debug_matches: bad argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const int32_t* src[4] = {h->pm_bi, h->pm_acc, h->wm_bi, h->wm_acc};
+  if (h->n_obs) HIP_TRY(hipMemcpy(dst, src[which], (size_t)h->n_obs * 4, hipMemcpyDeviceToHost));
   return PICP_OK;
 }
 

@@ -290,6 +290,10 @@ int picp_vo_get_map(picp_vo_t* h, int seg, int64_t cap, float* xyz, float* desc,
 /* mean device time of `reps` back-to-back runs (HIP events on the handle's stream) */
 int picp_vo_time(picp_vo_t* h, int reps, float* ms_per_run);
 int picp_vo_info(picp_vo_t* h, int64_t* n_obs, int64_t* n_slots, int64_t* map_slots, int* npt);
+/* Diagnostic: the last run's match outputs per observation (n_obs int32): which = 0 frame->next
+ * best index, 1 its accept flag, 2 frame->map best index, 3 its accept flag.  Best indices are
+ * defined only where the flag is 1 (the sequence runs the matcher's accept-only form). */
+int picp_vo_debug_matches(picp_vo_t* h, int which, int32_t* dst);
 
 /* ---------------- self-test ---------------- */
 /* The projection's reciprocal 1/z must be the correctly rounded one (src/camera.h:30; the

@@ -1,0 +1,7 @@
+#!/bin/bash
+export TMPDIR=/tmp
+mkdir -p gpurun_out/cs
+for sk in 0 4 2 6 1 5 8; do
+  PICP_VO_DIAG_SKIP=$sk timeout -k 10 120 python -u tools/conc_skip.py >> gpurun_out/cs/log 2>&1 || { echo "skip $sk failed"; tail -5 gpurun_out/cs/log; exit 1; }
+done
+grep skip= gpurun_out/cs/log
