@@ -1,4 +1,5 @@
 #!/bin/bash
+# Which VO kernel kind perturbs a block-mode batch beside it (tools/conc_skip.py per PICP_VO_DIAG_SKIP value).
 export TMPDIR=/tmp
 mkdir -p gpurun_out/cs
 for sk in 0 4 2 6 1 5 8; do

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round-2 profiles of the bench configs: rocprofv3 kernel-trace/stats per workload, then the HBM
 # traffic counters FETCH_SIZE and WRITE_SIZE in SEPARATE --pmc passes (MI355X_MICROARCH.md).
-# Every step time-limited; stop at the first failure.  OUT=gpurun_out/prof_r02
+# Every step time-limited; stop at the first failure.  OUT=${OUT:-gpurun_out/prof_r02}
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_r02
+OUT=${OUT:-gpurun_out/prof_r02}
 mkdir -p $OUT
 for W in ${WLS:-c2 c4 c3 c5}; do
   ARGS="--no-cpu --skip-extras --steps 10 --warmup 2 --workload $W"

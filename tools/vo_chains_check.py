@@ -1,5 +1,5 @@
 """Determinism check of the VO step scheduling (PICP_VO_CHAINS / OVERLAP / GRAPH / PRIO): the
-same synthetic sequence run under each setting must give bit-identical poses and step records.
+same synthetic sequence run under each setting, compared bit for bit with the first.
 usage: python tools/vo_chains_check.py FRAMES[:OBS[:SEED]] "ENV=V,ENV=V" ...   (first = reference)"""
 import os
 import sys
