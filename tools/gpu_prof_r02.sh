@@ -9,7 +9,7 @@ for W in ${WLS:-c2 c4 c3 c5}; do
   ARGS="--no-cpu --skip-extras --steps 10 --warmup 2 --workload $W"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/${W}_trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/${W}_trace.log 2>&1 || { echo "trace $W failed"; tail $OUT/${W}_trace.log; exit 1; }
   cp $OUT/${W}_trace/run_kernel_stats.csv $OUT/kernel_stats_$W.csv
-  python3 -c "import json; d=json.loads(open('$OUT/${W}_trace.log').read().strip().splitlines()[-1]); print('$W', d['value'], d['unit'], d['ms_per_step'])"
+  python3 -c "import json; d=json.loads([l for l in open('$OUT/${W}_trace.log').read().splitlines() if l.startswith('{')][-1]); print('$W', d['value'], d['unit'], d['ms_per_step'])"
 done
 for P in ${PMCS:-c2:c2_persistent:picp_persistent c4:c4x1024_block:picp_block c3:c3_persistent:picp_persistent}; do
   W=${P%%:*}; R=${P#*:}; NAME=${R%%:*}; K=${R#*:}
