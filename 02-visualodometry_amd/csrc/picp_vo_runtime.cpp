@@ -46,6 +46,17 @@ static_assert(sizeof(picp_vo_step) == sizeof(VoStep), "picp_vo_step must mirror 
 #define VO_MATCH_RATIO 0.8f  // RATIO_THRESHOLD, src/my_utilities.h:46
 #define VO_MAX_GRID_Y 65535
 
+// Diagnostic (PICP_VO_GUARD=1, read at create): every device buffer of the handle gets a
+// VO_GUARD-byte pattern-filled pad before and after it; picp_vo_debug_guard counts pad bytes that
+// no longer hold the pattern (an out-of-bounds store into or out of the buffer).
+#define VO_GUARD (1 << 20)
+#define VO_GUARD_BYTE 0xA5
+struct VoGuarded {
+  char* base;
+  size_t bytes;
+  const char* name;
+};
+
 struct picp_vo {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -98,7 +109,35 @@ struct picp_vo {
   std::vector<hipEvent_t> ev_cj;     // [chains]: group c's end (join), [0]: fork
   std::vector<hipEvent_t> ev_ph;     // [chains]: group c's first world match done
   int accept_only = 1;  // the sequence reads only accepted matches (PICP_VO_MATCH_FULL=1: full form)
+  bool guard = false;
+  std::vector<VoGuarded> guards;
 };
+
+
+static hipError_t vo_malloc(picp_vo* h, void** p, size_t bytes, const char* name) {
+  if (!h->guard) return hipMalloc(p, bytes);
+  char* base = nullptr;
+  hipError_t e = hipMalloc((void**)&base, bytes + 2 * (size_t)VO_GUARD);
+  if (e != hipSuccess) return e;
+  e = hipMemset(base, VO_GUARD_BYTE, bytes + 2 * (size_t)VO_GUARD);
+  if (e != hipSuccess) return e;
+  h->guards.push_back(VoGuarded{base, bytes, name});
+  *p = base + VO_GUARD;
+  return hipSuccess;
+}
+
+static void vo_dfree(picp_vo* h, void* p) {
+  if (!h->guard) {
+    hipFree(p);
+    return;
+  }
+  for (size_t i = 0; i < h->guards.size(); ++i)
+    if (h->guards[i].base + VO_GUARD == (char*)p) {
+      hipFree(h->guards[i].base);
+      h->guards.erase(h->guards.begin() + (long)i);
+      return;
+    }
+}
 
 static void vo_free_segments(picp_vo* h) {
   if (h->exec) hipGraphExecDestroy(h->exec);
@@ -108,7 +147,7 @@ static void vo_free_segments(picp_vo* h) {
   for (hipEvent_t e : h->ev_chunk)
     if (e) hipEventDestroy(e);
   h->ev_chunk.clear();
-  if (h->seg_mem) hipFree(h->seg_mem);
+  if (h->seg_mem) vo_dfree(h, h->seg_mem);
   h->seg_mem = nullptr;
   h->n_seg = 0;
 }
@@ -120,7 +159,7 @@ extern "C" int picp_vo_destroy(picp_vo_t* h) {
   void* bufs[] = {h->frame_off_d, h->uv_d, h->desc_d, h->pm_bi, h->pm_acc, h->wm_bi, h->wm_acc,
                   h->pm_bd, h->pm_sd, h->wm_bd, h->wm_sd, h->obs_h, h->obs_n1, h->obs_n2};
   for (void* p : bufs)
-    if (p) hipFree(p);
+    if (p) vo_dfree(h, p);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
@@ -188,8 +227,9 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
       return rc_;                 \
     }                             \
   } while (0)
+  if (const char* e = getenv("PICP_VO_GUARD")) h->guard = atoi(e) != 0;
   auto alloc = [&](void** p, size_t bytes) -> int {
-    HIP_TRY(hipMalloc(p, bytes));
+    HIP_TRY(vo_malloc(h, p, bytes, "create"));
     return PICP_OK;
   };
   VO_TRY([&]() -> int {
@@ -321,7 +361,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_mh = part((size_t)map_slots * h->dp * sizeof(_Float16));
   const Part p_mn1 = part((size_t)map_slots * sizeof(float));
   const Part p_mn2 = part((size_t)map_slots * sizeof(float));
-  HIP_TRY(hipMalloc(&h->seg_mem, total));
+  HIP_TRY(vo_malloc(h, &h->seg_mem, total, "segments"));
   HIP_TRY(hipMemset(h->seg_mem, 0, total));  // every table defined before the first run
   char* m = (char*)h->seg_mem;
   h->ev_chunk.assign((size_t)max_steps, nullptr);
@@ -561,6 +601,27 @@ extern "C" int picp_vo_debug_matches(picp_vo_t* h, int which, int32_t* dst) {
   HIP_TRY(hipDeviceSynchronize());
   const int32_t* src[4] = {h->pm_bi, h->pm_acc, h->wm_bi, h->wm_acc};
   if (h->n_obs) HIP_TRY(hipMemcpy(dst, src[which], (size_t)h->n_obs * 4, hipMemcpyDeviceToHost));
+  return PICP_OK;
+}
+
+extern "C" int picp_vo_debug_guard(picp_vo_t* h, int64_t* bad_bytes, int* bad_buffer) {
+  CHECK_ARG(h && bad_bytes && bad_buffer, "picp_vo_debug_guard: bad argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  *bad_bytes = 0;
+  *bad_buffer = -1;
+  std::vector<unsigned char> pad(VO_GUARD);
+  for (size_t i = 0; i < h->guards.size(); ++i) {
+    const VoGuarded& g = h->guards[i];
+    for (int side = 0; side < 2; ++side) {
+      const char* src = side ? g.base + VO_GUARD + g.bytes : g.base;
+      HIP_TRY(hipMemcpy(pad.data(), src, VO_GUARD, hipMemcpyDeviceToHost));
+      int64_t bad = 0;
+      for (unsigned char c : pad) bad += (c != VO_GUARD_BYTE);
+      if (bad && *bad_buffer < 0) *bad_buffer = (int)(2 * i + side);
+      *bad_bytes += bad;
+    }
+  }
   return PICP_OK;
 }
 

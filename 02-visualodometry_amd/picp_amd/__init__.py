@@ -42,7 +42,7 @@ EXPORTED = [
     "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_time_single",
     "picp_batch_info", "picp_batch_residency",
     "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
-    "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async", "picp_vo_debug_matches",
+    "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async", "picp_vo_debug_matches", "picp_vo_debug_guard",
     "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
     "picp_vo_info", "picp_selftest_rcp", "picp_essential_params_default", "picp_essential_batch",
     "picp_shard_range", "picp_comm_unique_id", "picp_comm_create", "picp_comm_destroy", "picp_comm_info",
@@ -142,6 +142,7 @@ def lib():
         "picp_vo_run": ([vp], i),
         "picp_vo_run_async": ([vp], i),
         "picp_vo_debug_matches": ([vp, i, ctypes.POINTER(ctypes.c_int32)], i),
+        "picp_vo_debug_guard": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i)], i),
         "picp_vo_sync": ([vp], i),
         "picp_vo_get_poses": ([vp, fp], i),
         "picp_vo_get_steps": ([vp, ctypes.POINTER(VOStep)], i),

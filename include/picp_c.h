@@ -294,6 +294,10 @@ int picp_vo_info(picp_vo_t* h, int64_t* n_obs, int64_t* n_slots, int64_t* map_sl
  * best index, 1 its accept flag, 2 frame->map best index, 3 its accept flag.  Best indices are
  * defined only where the flag is 1 (the sequence runs the matcher's accept-only form). */
 int picp_vo_debug_matches(picp_vo_t* h, int which, int32_t* dst);
+/* Diagnostic: with PICP_VO_GUARD=1 at create, every device buffer of the handle is bracketed by
+ * 1 MiB pads of a fixed pattern; *bad_bytes = pad bytes that changed, *bad_buffer = 2 * (buffer
+ * index in allocation order) + (0 before / 1 after) of the first changed pad, or -1. */
+int picp_vo_debug_guard(picp_vo_t* h, int64_t* bad_bytes, int* bad_buffer);
 
 /* ---------------- self-test ---------------- */
 /* The projection's reciprocal 1/z must be the correctly rounded one (src/camera.h:30; the
