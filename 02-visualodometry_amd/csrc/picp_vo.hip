@@ -275,7 +275,16 @@ __global__ __launch_bounds__(VOA_BLOCK) void vo_append_kernel(const VoArgs a, in
     const int2 pr = pairs[k];
     const int64_t slot = mbase + k;
     float o[3];
+#ifdef VOA_DIAG_NOTRI  // diagnostic build only (wrong map points): no FP64 triangulation
+    {
+      const float2 ua = a.uv[oc + pr.x], ub = a.uv[on + pr.y];
+      o[0] = ua.x * sP[0] + ub.x;
+      o[1] = ua.y * sP[5] + ub.y;
+      o[2] = 1.0f + sP[10];
+    }
+#else
     triangulate_dlt(sP, sP + 12, a.uv[oc + pr.x], a.uv[on + pr.y], o);
+#endif
     // the descriptor row and the matcher's prepped row of it (fp16 + guard norms): every load
     // first, then the stores -- the compiler cannot rule out that a store aliases a later load,
     // so an interleaved element copy paid one global round trip per element
