@@ -632,6 +632,23 @@ __device__ __forceinline__ void bfly_dpp(float* v, int lane) {
 // is the pair sum of the half each lane keeps.  Returns, in every lane, the wave total of value
 // index (lane >> 1).
 __device__ __forceinline__ float wave_reduce32(float* v, int lane) {
+#ifdef PICP_NO_PERMLANE_SWAP
+  // the half-wave exchanges through ds_bpermute (bit-identical sums in the same order).  Results
+  // of the v_permlane*_swap form below moved in the last bits when other kernels ran beside it on
+  // MI355X; this form did not.  Costs C2 3 %, C4 15 %, C5 10 %.
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool hi = (lane & 32) != 0;
+    const float send = hi ? v[i] : v[i + 16], keep = hi ? v[i + 16] : v[i];
+    v[i] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool hi = (lane & 16) != 0;
+    const float send = hi ? v[i] : v[i + 8], keep = hi ? v[i + 8] : v[i];
+    v[i] = keep + __shfl_xor(send, 16);
+  }
+#else
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 16]), false, false);
@@ -642,6 +659,7 @@ __device__ __forceinline__ float wave_reduce32(float* v, int lane) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
     v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
+#endif
   bfly_dpp<DPP_ROW_MIRROR, 3, 4>(v, lane);
   bfly_dpp<DPP_ROW_HALF_MIRROR, 2, 2>(v, lane);
   bfly_dpp<DPP_QUAD_XOR2, 1, 1>(v, lane);

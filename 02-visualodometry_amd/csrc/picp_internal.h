@@ -74,7 +74,10 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 // Diagnostic build only (-DPICP_KFENCE): explicit agent-scope acquire at the start and release at
 // the end of the VO path's kernels, to test whether kernel-boundary visibility is what differs
 // between schedules.
-#ifdef PICP_KFENCE
+#if defined(PICP_KFENCE_SYS)  // system scope: also writes back / invalidates the XCD's L2
+#define PICP_KFENCE_IN() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "")
+#define PICP_KFENCE_OUT() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "")
+#elif defined(PICP_KFENCE)
 #define PICP_KFENCE_IN() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
 #define PICP_KFENCE_OUT() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
 #else
