@@ -48,8 +48,12 @@ def test_c4_full_batch_every_frame_vs_oracle(native, oracle, conv):
     errs = np.array([synth.se3_log_norm(P[i], ref[i][0]) for i in range(F)])
     dn = np.array([abs(S[i]["n_in"] - ref[i][1]["n_in"]) for i in range(F)])
     assert errs.max() < POSE_TOL, (errs.max(), int(errs.argmax()))
-    assert dn.max() <= 2, (dn.max(), int(dn.argmax()))
     assert (dn == 0).mean() > 0.9
+    from test_gpu_parity import _assert_n_in_explained
+    off = np.concatenate([[0], np.cumsum(bt["sizes"])])
+    for i in np.flatnonzero(dn):  # every n_in difference covered by threshold-ambiguous points
+        sl = slice(int(off[i]), int(off[i + 1]))
+        _assert_n_in_explained(bt["K"], bt["xyz"][sl], bt["uv"][sl], P[i], ref[i][0], S[i]["n_in"], ref[i][1]["n_in"])
     rounds = np.array([S[i]["rounds"] for i in range(F)])
     ref_rounds = np.array([ref[i][1]["rounds"] for i in range(F)])
     if conv < 0:
