@@ -149,6 +149,7 @@ for r in range(6):
     P = vo.poses()
     mv.append("=" if all(np.array_equal(x.view(np.uint32), y.view(np.uint32)) for x, y in zip(P, ref_v)) else "X")
 print("%-28s %s" % ("batch beside VO", " ".join(mb)), flush=True)
+print("batch residency after the VO pairs:", B.residency() if hasattr(B, "residency") else None, "info", B.info(), flush=True)
 print("%-28s %s" % ("VO beside batch", " ".join(mv)), flush=True)
 
 # the batch beside the matcher alone (a thread looping the batched matcher; ctypes drops the GIL)
