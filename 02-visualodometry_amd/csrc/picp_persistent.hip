@@ -52,6 +52,15 @@ __device__ __forceinline__ unsigned long long granule(unsigned epoch, float v) {
   return ((unsigned long long)epoch << 32) | (unsigned long long)__float_as_uint(v);
 }
 
+// hand-off polls run back to back: an s_sleep 1 (64 clocks) between polls measured C2 214-223k
+// vs 222-225k it/s without it, bimodal vs steady (C3 unchanged; profiles/r02/e3/ab_spin.log).
+// -DPICP_POLL_SLEEP restores the pause for A/B runs.
+#ifdef PICP_POLL_SLEEP
+#define PICP_POLL_PAUSE() __builtin_amdgcn_s_sleep(1)
+#else
+#define PICP_POLL_PAUSE() ((void)0)
+#endif
+
 __device__ __forceinline__ bool timed_out(unsigned long long deadline) {
   return __builtin_amdgcn_s_memrealtime() > deadline;
 }
@@ -216,7 +225,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
           s_tmo = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        PICP_POLL_PAUSE();
       }
       double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
@@ -315,7 +324,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
             if (lane < 12) gp = __float_as_uint(s_pose[lane]);
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+          PICP_POLL_PAUSE();
         }
         if (lane < 12) s_pose[lane] = __uint_as_float((unsigned)gp);
         if (lane == 12) s_done = (int)(unsigned)gp;
