@@ -32,6 +32,14 @@ using namespace picp;
 
 #define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs (split 1, 2); 256 for split 4
 #define PICP_BLDS_ITEMS 7680  // items staged in LDS: 5 x 4 B x 7680 = 150 KB of the 160 KB per CU
+// partner polls run back to back: an s_sleep 1 between polls measured C4 1704-1711 us vs
+// 1700-1706 us without it, 4 of 4 interleaved reps (profiles/r02/e4/ab_bspin.log).
+// -DPICP_BPOLL_SLEEP restores the pause for A/B runs.
+#ifdef PICP_BPOLL_SLEEP
+#define PICP_BPOLL_PAUSE() __builtin_amdgcn_s_sleep(1)
+#else
+#define PICP_BPOLL_PAUSE() ((void)0)
+#endif
 #define PICP_XG 64            // exchange granules per block per round: 32 hi + 32 lo
 
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
             s_tmo = 1;
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+          PICP_BPOLL_PAUSE();
         }
         t = part_t[0];
 #pragma unroll
