@@ -1,7 +1,8 @@
 // Diagnostic only: fill every CU's LDS and a wave's worth of VGPRs
 // with a fixed bit pattern, then exit.  A solve launched after it (serially) that reads state it
 // never wrote sees the pattern; comparing solves after two patterns rules stale-state reads in or
-// out.  Not on the product path; built by tools/gpu_poison.sh into tools/_build/libpoison.so.
+// out.  Not on the product path.  Build on the CPU before the gpurun call:
+//   hipcc -O3 --offload-arch=gfx950 -shared -fPIC tools/poison.hip -o tools/_build/libpoison.so
 #include <hip/hip_runtime.h>
 
 #define POISON_LDS_WORDS (160 * 1024 / 4)
