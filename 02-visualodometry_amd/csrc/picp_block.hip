@@ -64,6 +64,47 @@ extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words
   } while (0)
 #endif
 
+// Diagnostic build only (-DPICP_BDIAG, tools/bdiag_check.py, tools/bdiag_vo.py): per (problem,
+// round), the pose each wave linearized at, the 8 wave sums of every term, the converted totals,
+// the finishing wave's new pose, a lane-agreement count of the finishing wave, per wave the lanes
+// whose permlane/DPP reduction differs from the ds_bpermute form of the same sums, and an XOR
+// checksum of the problem's inputs.  Batch mode: a uniform split-1 batch of picp_bdiag_nprob
+// problems, record (problem, round).  VO mode (picp_bdiag_cap > 0): the sequence's launches,
+// record (segment = offset / cap, launch count of that segment, round).
+#ifdef PICP_BDIAG
+#ifndef PICP_BDIAG_PARTS
+#define PICP_BDIAG_PARTS 15  // 1 input checksum, 2 wave poses, 4 wave sums + totals, 8 finish
+#endif
+#define BDIAG_REC 576  // [448 + 50 j]: finish of lane 0 (j 0) / lane 48 (j 1): 32 totals, dx, R t;
+                       // [416 + 2w]: lanes of wave w whose pose differs from lane 0's; [432]: same, finish;
+                       // [434..439]: finish inputs that differ from lane 0's: s_tot words, pose, chi_prev
+__device__ float* picp_bdiag_buf;
+__device__ int picp_bdiag_nprob;
+__device__ int picp_bdiag_rounds;
+__device__ long long picp_bdiag_cap;
+__device__ int picp_bdiag_nseg;
+__device__ int picp_bdiag_steps;
+__device__ unsigned picp_bdiag_cnt[4096];
+__device__ float* picp_bdiag_lane;  // part 16: VO step 0, [segment][round][wave][lane][32] folded partials
+extern "C" hipError_t picp_debug_bdiag_lane(float* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_lane), &buf, sizeof(buf));
+}
+extern "C" hipError_t picp_debug_bdiag_set(float* buf, int n_problems, int rounds, long long cap, int nseg,
+                                           int steps) {
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_buf), &buf, sizeof(buf));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_nprob), &n_problems, sizeof(int));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_rounds), &rounds, sizeof(int));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_cap), &cap, sizeof(cap));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_nseg), &nseg, sizeof(int));
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_steps), &steps, sizeof(int));
+  static const unsigned zero[4096] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_cnt), zero, sizeof(zero));
+  return e;
+}
+#define BDIAG_ON (s_diag != nullptr && round <= picp_bdiag_rounds)
+#define BDIAG_PTR (s_diag + (size_t)(round - 1) * BDIAG_REC)
+#endif
+
 template <int NPT, int PH, int BS>
 __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
@@ -105,6 +146,27 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     n = min(n, first + part) - first;
     if (n > 0) base += first;  // an empty part keeps a valid base (its loads are clamped to it)
   }
+#ifdef PICP_BDIAG
+  __shared__ float* s_diag;
+  __shared__ float* s_ldiag;
+  if (tid == 0) {
+    float* d = nullptr;
+    s_ldiag = nullptr;
+    if (picp_bdiag_buf && split == 1) {
+      if (picp_bdiag_cap > 0 && !A.uniform) {
+        const long long seg = base / picp_bdiag_cap;
+        const unsigned k = atomicAdd(&picp_bdiag_cnt[seg & 4095], 1u);
+        if (seg < picp_bdiag_nseg && (int)k < picp_bdiag_steps)
+          d = picp_bdiag_buf + ((size_t)seg * picp_bdiag_steps + k) * picp_bdiag_rounds * BDIAG_REC;
+        if (seg < picp_bdiag_nseg && k == 0 && picp_bdiag_lane)
+          s_ldiag = picp_bdiag_lane + (size_t)seg * picp_bdiag_rounds * BS * PICP_NPART;
+      } else if (picp_bdiag_cap == 0 && A.uniform && n_problems == picp_bdiag_nprob) {
+        d = picp_bdiag_buf + (size_t)p * picp_bdiag_rounds * BDIAG_REC;
+      }
+    }
+    s_diag = d;
+  }
+#endif
   bgu64_t* const xgg = (bgu64_t*)xg;
   // split: exchange tags are tbase + round, tbase = the rounds this grid slot ran in earlier
   // launches on these buffers (partners run identical solves, so their bases stay equal); stale
@@ -159,6 +221,17 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     s_st = s;
   }
   __syncthreads();
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 1)
+  if (s_diag) {  // XOR of the bits of every input item (order-free), and n
+    unsigned x = 0;
+    for (int i = tid; i < n; i += BS)
+      x ^= __float_as_uint(X[base + i]) ^ (__float_as_uint(Y[base + i]) * 3u) ^ (__float_as_uint(Z[base + i]) * 5u) ^
+           (__float_as_uint(U[base + i]) * 7u) ^ (__float_as_uint(V[base + i]) * 11u);
+    for (int o = 32; o > 0; o >>= 1) x ^= (unsigned)__shfl_xor((int)x, o);
+    if (lane == 0) atomicXor(reinterpret_cast<unsigned*>(s_diag + 413), x);
+    if (tid == 0) s_diag[414] = (float)n;
+  }
+#endif
 
   Cam C;
   C.k00 = A.K[0]; C.k10 = A.K[1]; C.k20 = A.K[2];
@@ -180,6 +253,27 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
     T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 32)
+    if (BDIAG_ON) {  // lanes whose pose differs from lane 0's (the pose every lane linearizes at)
+      const float tv[12] = {T.r00, T.r10, T.r20, T.r01, T.r11, T.r21, T.r02, T.r12, T.r22, T.t0, T.t1, T.t2};
+      bool mism = false;
+#pragma unroll
+      for (int i = 0; i < 12; ++i)
+        mism |= __float_as_int(tv[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(tv[i]));
+      const unsigned long long mm = __ballot(mism);
+      if (lane == 0 && mm) {
+        BDIAG_PTR[416 + 2 * wave] = __uint_as_float((unsigned)mm);
+        BDIAG_PTR[417 + 2 * wave] = __uint_as_float((unsigned)(mm >> 32));
+      }
+    }
+#endif
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 2)
+    if (BDIAG_ON && lane == 0) {
+      float* d = BDIAG_PTR + wave * 12;
+      d[0] = T.r00; d[1] = T.r10; d[2] = T.r20; d[3] = T.r01; d[4] = T.r11; d[5] = T.r21;
+      d[6] = T.r02; d[7] = T.r12; d[8] = T.r22; d[9] = T.t0; d[10] = T.t1; d[11] = T.t2;
+    }
+#endif
     Acc2 a;
     acc2_zero(a);
     Cnt nr = {0u, 0u}, nd = {0u, 0u};  // counts: register items (uniform), divergent loops (lane 0)
@@ -203,7 +297,27 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     float v[PICP_NPART];
     BSTAMP(1);
     acc2_fold(a, v);
-    const float wsum = wave_counts(wave_reduce32(v, lane), lane, (Cnt){nr.n_in + nd.n_in, nr.n_proj + nd.n_proj});
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 16)
+    if (s_ldiag && round <= picp_bdiag_rounds) {
+      float* d = s_ldiag + ((size_t)(round - 1) * BS + tid) * PICP_NPART;
+#pragma unroll
+      for (int i = 0; i < PICP_NPART; ++i) d[i] = v[i];
+    }
+#endif
+#if defined(PICP_BDIAG) && !defined(PICP_BDIAG_NOCHK)
+    float vchk[PICP_NPART];
+#pragma unroll
+    for (int i = 0; i < PICP_NPART; ++i) vchk[i] = v[i];
+    const float rchk = wave_reduce32_bperm(vchk, lane);
+#endif
+    const float wred = wave_reduce32(v, lane);
+#if defined(PICP_BDIAG) && !defined(PICP_BDIAG_NOCHK)
+    {
+      const int nbad = __popcll(__ballot(__float_as_int(rchk) != __float_as_int(wred)));
+      if (BDIAG_ON && lane == 0) BDIAG_PTR[405 + wave] = (float)nbad;
+    }
+#endif
+    const float wsum = wave_counts(wred, lane, (Cnt){nr.n_in + nd.n_in, nr.n_proj + nd.n_proj});
     if ((lane & 1) == 0) s_wave[lane >> 1][wave] = wsum;
     BSTAMP(2);
     __syncthreads();
@@ -220,6 +334,10 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       float ws[BS / 64];  // every load issued before the first add (one LDS wait)
 #pragma unroll
       for (int w = 0; w < BS / 64; ++w) ws[w] = s_wave[tid][w];
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 4)
+      if (BDIAG_ON && BS == 512)
+        for (int w = 0; w < 8; ++w) BDIAG_PTR[96 + tid * 8 + w] = ws[w];
+#endif
       double t = (double)ws[0];
 #pragma unroll
       for (int w = 1; w < BS / 64; ++w) t += (double)ws[w];
@@ -270,15 +388,114 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
           if (q < split) t += part_t[q];
       }
       s_tot[tid] = total_word(A, tid, t);  // lane e converts total e
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 4)
+      if (BDIAG_ON) BDIAG_PTR[352 + tid] = total_word(A, tid, t);
+#endif
     }
     // the totals (and s_tmo) were written by lanes < 32 of wave 0, which also runs the solve:
     // a wave barrier orders them, the other waves wait at the block barrier after the solve
+#ifdef PICP_FINISH_SYNC
+    __syncthreads();
+#else
     __builtin_amdgcn_wave_barrier();
+#endif
     BSTAMP(4);
     if (wave == 0) {  // the wave finishes the round (every lane the same values, state in registers)
       RoundOut o;
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 64)
+      if (BDIAG_ON) {  // which finish inputs differ across the wave's lanes
+        bool m_tot = false, m_pose = false;
+#pragma unroll
+        for (int i = 0; i < PICP_NPART; ++i) {
+          const float x = s_tot[i];
+          m_tot |= __float_as_int(x) != __builtin_amdgcn_readfirstlane(__float_as_int(x));
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) m_pose |= __float_as_int(pr[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pr[i]));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) m_pose |= __float_as_int(pt[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pt[i]));
+        const bool m_chi = __float_as_int(chi_prev) != __builtin_amdgcn_readfirstlane(__float_as_int(chi_prev));
+        const unsigned long long a = __ballot(m_tot), b = __ballot(m_pose), c = __ballot(m_chi);
+        if (lane == 0 && (a | b | c)) {
+          float* d = BDIAG_PTR;
+          d[434] = __uint_as_float((unsigned)a); d[435] = __uint_as_float((unsigned)(a >> 32));
+          d[436] = __uint_as_float((unsigned)b); d[437] = __uint_as_float((unsigned)(b >> 32));
+          d[438] = __uint_as_float((unsigned)c); d[439] = __uint_as_float((unsigned)(c >> 32));
+        }
+      }
+#endif
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 128)
+      {  // finish_round_pose restated with per-stage records of lanes 0 and 48
+        float twr[PICP_NPART];
+#pragma unroll
+        for (int i = 0; i < PICP_NPART; ++i) twr[i] = s_tot[i];
+        o.chi_in = twr[PICP_P_CHI_IN];
+        o.chi_out = twr[PICP_P_CHI_OUT];
+        o.n_in = __float_as_int(twr[PICP_P_N_IN]);
+        o.n_proj = __float_as_int(twr[PICP_P_N_PROJ]);
+        o.converged = 0;
+        float dx[6] = {0, 0, 0, 0, 0, 0};
+        if (o.n_in < A.min_inliers) {
+          o.ok = 0;
+          o.done = 1;
+        } else {
+          ldl6_solve(twr, dx);
+          apply_update(dx, pr, pt);
+          o.ok = 1;
+          o.done = 0;
+          const float prev = chi_prev, cur = o.chi_in;
+          const float rel = (prev > 1e-10f) ? fabsf(prev - cur) / prev : 0.0f;
+          if (rel < A.conv_eps) {
+            o.converged = 1;
+            o.done = 1;
+          } else {
+            chi_prev = cur;
+          }
+          if (round >= A.max_rounds) o.done = 1;
+        }
+        if (BDIAG_ON && (lane == 0 || lane == 48)) {
+          float* d = BDIAG_PTR + 448 + (lane == 48 ? 50 : 0);
+#pragma unroll
+          for (int i = 0; i < 32; ++i) d[i] = twr[i];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) d[32 + i] = dx[i];
+#pragma unroll
+          for (int i = 0; i < 9; ++i) d[38 + i] = pr[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) d[47 + i] = pt[i];
+        }
+      }
+#else
       finish_round_pose(A, s_tot, round, pr, pt, chi_prev, o);
+#endif
       if (s_tmo) o.done = 1;  // a partner wait timed out: stop (the host reports the error)
+#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 8)
+      if (BDIAG_ON) {
+        bool mism = false;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+          mism |= __float_as_int(pr[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pr[i]));
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          mism |= __float_as_int(pt[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pt[i]));
+        const unsigned long long mm = __ballot(mism);
+        const int nm = __popcll(mm);
+        if (lane == 0) {
+          float* d = BDIAG_PTR;
+          d[432] = __uint_as_float((unsigned)mm);
+          d[433] = __uint_as_float((unsigned)(mm >> 32));
+#pragma unroll
+          for (int i = 0; i < 9; ++i) d[384 + i] = pr[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) d[393 + i] = pt[i];
+          d[396] = o.chi_in;
+          d[397] = (float)o.n_in;
+          d[398] = (float)o.done;
+          d[399] = chi_prev;
+          d[404] = (float)nm;
+        }
+      }
+#endif
       if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];

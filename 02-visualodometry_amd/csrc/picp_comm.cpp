@@ -95,6 +95,25 @@ extern "C" int picp_shard_range(int64_t n_items, int world, int rank, int64_t* f
   return PICP_OK;
 }
 
+extern "C" int64_t picp_shard_pad(int64_t n_items, int world) {
+  if (n_items < 0 || world < 1) return -1;
+  return (n_items + world - 1) / world;
+}
+
+extern "C" int picp_shard_unpack(int64_t n_items, int world, int64_t item_bytes, const void* padded, void* out) {
+  CHECK_ARG(n_items >= 0 && world >= 1 && item_bytes >= 1, "picp_shard_unpack: bad size");
+  CHECK_ARG(n_items == 0 || (padded && out), "picp_shard_unpack: null buffer");
+  const int64_t pad = picp_shard_pad(n_items, world);
+  const char* src = (const char*)padded;
+  char* dst = (char*)out;
+  for (int r = 0; r < world; ++r) {
+    int64_t a = 0, e = 0;
+    picp_shard_range(n_items, world, r, &a, &e);
+    if (e > a) memcpy(dst + a * item_bytes, src + (size_t)r * pad * item_bytes, (size_t)(e - a) * item_bytes);
+  }
+  return PICP_OK;
+}
+
 extern "C" int picp_comm_unique_id(uint8_t id[PICP_COMM_ID_BYTES]) {
   CHECK_ARG(id, "picp_comm_unique_id: null output");
   static_assert(sizeof(ncclUniqueId) == PICP_COMM_ID_BYTES, "RCCL unique id size");

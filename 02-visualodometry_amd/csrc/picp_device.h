@@ -606,7 +606,11 @@ namespace picp {
 // lane inside a 16-lane row (row_mirror l^15, row_half_mirror l^7, quad_perm l^2, l^1).
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
+#ifdef PICP_DPP_OLD
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+#else
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+#endif
 }
 #define DPP_ROW_MIRROR 0x140
 #define DPP_ROW_HALF_MIRROR 0x141
@@ -631,6 +635,26 @@ __device__ __forceinline__ void bfly_dpp(float* v, int lane) {
 // half holds (own v[i], partner v[i]) and the high half (partner v[i+16], own v[i+16]), so a+b
 // is the pair sum of the half each lane keeps.  Returns, in every lane, the wave total of value
 // index (lane >> 1).
+__device__ __forceinline__ float wave_reduce32_bperm(float* v, int lane) {
+  // the half-wave exchanges through ds_bpermute (bit-identical sums in the same order)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool hi = (lane & 32) != 0;
+    const float send = hi ? v[i] : v[i + 16], keep = hi ? v[i + 16] : v[i];
+    v[i] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool hi = (lane & 16) != 0;
+    const float send = hi ? v[i] : v[i + 8], keep = hi ? v[i + 8] : v[i];
+    v[i] = keep + __shfl_xor(send, 16);
+  }
+  bfly_dpp<DPP_ROW_MIRROR, 3, 4>(v, lane);
+  bfly_dpp<DPP_ROW_HALF_MIRROR, 2, 2>(v, lane);
+  bfly_dpp<DPP_QUAD_XOR2, 1, 1>(v, lane);
+  return v[0] + dpp<DPP_QUAD_XOR1>(v[0]);
+}
+
 __device__ __forceinline__ float wave_reduce32(float* v, int lane) {
 #ifdef PICP_NO_PERMLANE_SWAP
   // the half-wave exchanges through ds_bpermute (bit-identical sums in the same order).  Results

@@ -769,24 +769,26 @@ extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* de
   return hipGetLastError();
 }
 
-// The pre-filtered match over prepped descriptors (picp_launch_match_prep), unless
-// PICP_MATCH_EXACT=1 selects the exact scan (same results; for A/B checks).
+// The pre-filtered match over prepped descriptors (picp_launch_match_prep).  form (include/picp_c.h
+// PICP_MATCH_FORM_*): bit 0 = the accept-only radius form (only accepted[] and the best index of
+// accepted queries are defined), bit 1 = the exact scan (the same results as the full form; for
+// A/B checks and the tests).
 extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
                                              const float* q_desc, const float* r_desc,
                                              const _Float16* q_h, const float* q_n1,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int accept_only) {
+                                             float* second_dist, int32_t* accepted, int form) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
+  const bool accept_only = (form & 1) != 0;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
   // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
   const bool rad = accept_only && dist_thr > 0.0f && dist_thr < 1e30f && ratio_thr > 0.0f && ratio_thr <= 1.0f;
   // the folded form needs the extension slots (dim <= 12) and tau/2 inside fp16 range
   const char* nf = getenv("PICP_MATCH_NO_FOLD");
   const bool fold = rad && dim <= 12 && (dist_thr / ratio_thr) <= 1000.0f && !(nf && atoi(nf) != 0);
-  const char* ex = getenv("PICP_MATCH_EXACT");
-  if (ex && atoi(ex) != 0)
+  if (form & 2)
     return picp_launch_match(stream, n_problems, max_nq, q_desc, r_desc, probs, dim, dist_thr, ratio_thr,
                              best_idx, best_dist, second_dist, accepted);
   // RB = 2 (64 queries per wave) halves the tile fetches and LDS B reads per query but also the

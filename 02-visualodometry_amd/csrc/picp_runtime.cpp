@@ -59,13 +59,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int accept_only);
-// PICP_MATCH_ACCEPT_ONLY=1 runs picp_match(_batch) in the matcher's accept-only form (what the
-// VO sequence uses) so the tests can check it against the oracle directly
-static int match_accept_only() {
-  const char* e = getenv("PICP_MATCH_ACCEPT_ONLY");
-  return (e && atoi(e) != 0) ? 1 : 0;
-}
+                                             float* second_dist, int32_t* accepted, int form);
 extern "C" int picp_match_prep_kch(int dim);
 extern "C" __global__ void picp_rcp_check_kernel(int e_lo, int e_hi, unsigned long long* bad);
 extern "C" hipError_t picp_launch_essential(hipStream_t stream, const EssArgs* args, const int64_t* offs,
@@ -396,6 +390,12 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
       }
       b->npt = bnpt;
     }
+  }
+  // report the hand-off grid of the layout in use only (a candidate the occupancy check rejected
+  // leaves no hand-off behind: picp_batch_residency then reads 0/0)
+  if (!(b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1))) {
+    b->handoff_grid = 0;
+    b->handoff_resident = 0;
   }
   b->ipb = ipb;
   b->vec = (ipb >= 4 * PICP_BLOCK && b->mode == PICP_MODE_GRAPH) ? 4 : 1;
@@ -885,35 +885,44 @@ extern "C" int picp_batch_time(picp_batch_t* b, const picp_params* prm, int reps
                                float* total_ms, float* launch_us) {
   CHECK_ARG(b && prm && reps > 0, "picp_batch_time: bad argument");
   HIP_TRY(hipSetDevice(b->device));
-  int rc = batch_upload_params(b, prm);
-  if (rc) return rc;
-  const int R = prm->max_rounds;
-  if (b->mode == PICP_MODE_GRAPH) {
-    rc = ensure_graph(b, R);  // captured before the timed region
+  // A hand-off wait that timed out inside the region is only seen by batch_read_results after
+  // it, which re-runs the solve without hand-offs (fallbacks + 1).  The region's time then
+  // includes the timed-out launches, so it is measured once more under the new layout.
+  for (int attempt = 0;; ++attempt) {
+    int rc = batch_upload_params(b, prm);
     if (rc) return rc;
+    const int R = prm->max_rounds;
+    if (b->mode == PICP_MODE_GRAPH) {
+      rc = ensure_graph(b, R);  // captured before the timed region
+      if (rc) return rc;
+    }
+    EventPair ev;
+    HIP_TRY(ev.create());
+    HIP_TRY(persistent_tag_guard(b, R, reps));
+    HIP_TRY(hipEventRecord(ev.a, b->stream));
+    for (int r = 0; r < reps; ++r) {
+      rc = enqueue_fused(b, R);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(ev.b, b->stream));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    if (total_ms) *total_ms = ms;
+    b->last_rounds = R;
+    b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
+    b->last_persistent = uses_err_word(b);
+    // mean launch period of the dominant kernel inside the region (graph mode: R round launches
+    // per solve; otherwise one launch per solve); back-to-back launches, so this is the
+    // per-launch duration a kernel trace reports plus the boundary gap
+    const int launches = (b->mode == PICP_MODE_GRAPH) ? std::max(R, 1) : 1;
+    if (launch_us) *launch_us = 1000.0f * ms / (float)(reps * launches);
+    const int fb0 = b->fallbacks;
+    rc = batch_read_results(b);
+    if (rc || b->fallbacks == fb0) return rc;
+    if (attempt >= 1)
+      return set_err(PICP_ERR_STATE, "picp_batch_time: hand-off waits timed out again after the fallback");
   }
-  EventPair ev;
-  HIP_TRY(ev.create());
-  HIP_TRY(persistent_tag_guard(b, R, reps));
-  HIP_TRY(hipEventRecord(ev.a, b->stream));
-  for (int r = 0; r < reps; ++r) {
-    rc = enqueue_fused(b, R);
-    if (rc) return rc;
-  }
-  HIP_TRY(hipEventRecord(ev.b, b->stream));
-  HIP_TRY(hipEventSynchronize(ev.b));
-  float ms = 0.0f;
-  HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
-  if (total_ms) *total_ms = ms;
-  b->last_rounds = R;
-  b->result_idx = (b->mode == PICP_MODE_GRAPH) ? graph_result_idx(R) : 0;
-  b->last_persistent = uses_err_word(b);
-  // mean launch period of the dominant kernel inside the region (graph mode: R round launches
-  // per solve; otherwise one launch per solve); back-to-back launches, so this is the per-launch
-  // duration a kernel trace reports plus the boundary gap
-  const int launches = (b->mode == PICP_MODE_GRAPH) ? std::max(R, 1) : 1;
-  if (launch_us) *launch_us = 1000.0f * ms / (float)(reps * launches);
-  return batch_read_results(b);
 }
 
 extern "C" int picp_batch_time_single(picp_batch_t* b, const picp_params* prm, float* us) {
@@ -974,36 +983,44 @@ extern "C" int picp_batch_residency(picp_batch_t* b, int* grid, int* resident, i
 // copy to the host give every rank all n_total poses and stats in problem order.
 extern "C" int picp_batch_allgather(picp_batch_t* b, picp_comm_t* c, int64_t n_total, float* T_all,
                                     picp_stats* st_all) {
-  CHECK_ARG(b && c && T_all, "picp_batch_allgather: null argument");
-  CHECK_ARG(picp_comm_device(c) == b->device, "picp_batch_allgather: communicator and batch are on different devices");
+  CHECK_ARG(c, "picp_batch_allgather: null communicator");
   const int world = picp_comm_world(c), rank = picp_comm_rank(c);
+  // Local checks first, agreed on by every rank before the collective: a rank that returned here
+  // alone would leave the others blocked in the all-gather.
+  int rc = PICP_OK;
   int64_t f0 = 0, f1 = 0;
-  int rc = picp_shard_range(n_total, world, rank, &f0, &f1);
-  if (rc) return rc;
-  CHECK_ARG(f1 - f0 == b->np, "picp_batch_allgather: the batch does not hold this rank's shard of n_total");
-  HIP_TRY(hipSetDevice(b->device));
-  rc = batch_read_results(b);  // the solve is complete (re-run if a hand-off timed out)
-  if (rc) return rc;
-  const int64_t maxn = (n_total + world - 1) / world;
-  const size_t bytes = (size_t)std::max<int64_t>(maxn, 1) * sizeof(PicpState);
-  void* send = picp_comm_send_buffer(c, bytes);
-  if (!send) return set_err(PICP_ERR_NOMEM, "picp_batch_allgather: staging buffer of %zu B", bytes);
+  void* send = nullptr;
+  const int64_t maxn = std::max<int64_t>(picp_shard_pad(n_total, world), 1);
+  const size_t bytes = (size_t)maxn * sizeof(PicpState);
+  if (!b || !T_all) rc = set_err(PICP_ERR_ARG, "picp_batch_allgather: null argument");
+  else if (picp_comm_device(c) != b->device)
+    rc = set_err(PICP_ERR_ARG, "picp_batch_allgather: communicator and batch are on different devices");
+  else if ((rc = picp_shard_range(n_total, world, rank, &f0, &f1)) == PICP_OK && f1 - f0 != b->np)
+    rc = set_err(PICP_ERR_ARG, "picp_batch_allgather: the batch does not hold this rank's shard of n_total");
+  if (rc == PICP_OK && hipSetDevice(b->device) != hipSuccess)
+    rc = set_err(PICP_ERR_DEVICE, "picp_batch_allgather: hipSetDevice failed");
+  if (rc == PICP_OK) rc = batch_read_results(b);  // the solve is complete (re-run if a hand-off timed out)
+  if (rc == PICP_OK && !(send = picp_comm_send_buffer(c, bytes)))
+    rc = set_err(PICP_ERR_NOMEM, "picp_batch_allgather: staging buffer of %zu B", bytes);
+  double fail = (rc == PICP_OK) ? 0.0 : 1.0;
+  const std::string local_err = rc ? picp_last_error() : "";
+  const int rc2 = picp_comm_allreduce_max(c, &fail, 1);
+  if (rc) return set_err(rc, "%s", local_err.c_str());
+  if (rc2) return rc2;
+  if (fail != 0.0) return set_err(PICP_ERR_STATE, "picp_batch_allgather: another rank failed before the all-gather");
   HIP_TRY(hipMemcpyAsync(send, b->st_d[b->result_idx], (size_t)b->np * sizeof(PicpState), hipMemcpyDeviceToDevice,
                          b->stream));
   const void* recv = nullptr;
   rc = picp_comm_allgather_dev(c, send, bytes, b->stream, &recv);
   if (rc) return rc;
-  std::vector<PicpState> all((size_t)world * std::max<int64_t>(maxn, 1));
-  HIP_TRY(hipMemcpyAsync(all.data(), recv, all.size() * sizeof(PicpState), hipMemcpyDeviceToHost, b->stream));
+  std::vector<PicpState> padded((size_t)world * maxn), all((size_t)std::max<int64_t>(n_total, 1));
+  HIP_TRY(hipMemcpyAsync(padded.data(), recv, padded.size() * sizeof(PicpState), hipMemcpyDeviceToHost, b->stream));
   HIP_TRY(hipStreamSynchronize(b->stream));
-  for (int r = 0; r < world; ++r) {
-    int64_t a = 0, e = 0;
-    picp_shard_range(n_total, world, r, &a, &e);
-    for (int64_t k = 0; k < e - a; ++k) {
-      const PicpState& st = all[(size_t)r * maxn + k];
-      state_to_pose(st, T_all + 16 * (a + k));
-      if (st_all) state_to_stats(st, st_all[a + k]);
-    }
+  rc = picp_shard_unpack(n_total, world, sizeof(PicpState), padded.data(), all.data());
+  if (rc) return rc;
+  for (int64_t k = 0; k < n_total; ++k) {
+    state_to_pose(all[(size_t)k], T_all + 16 * k);
+    if (st_all) state_to_stats(all[(size_t)k], st_all[k]);
   }
   return PICP_OK;
 }
@@ -1457,10 +1474,12 @@ extern "C" int picp_essential_batch(int device, int n_problems, const int64_t* o
 // ------------------------------------------------------------------------------------
 // descriptor matching (match_points, src/my_utilities.h:70-120)
 // ------------------------------------------------------------------------------------
-extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1, const int64_t* off2,
-                                const float* desc1, const float* desc2, int dim, float dist_thr,
-                                float ratio_thr, int32_t* best_idx, float* best_dist,
-                                float* second_dist, int32_t* accepted) {
+extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* off1, const int64_t* off2,
+                                     const float* desc1, const float* desc2, int dim, float dist_thr,
+                                     float ratio_thr, int32_t* best_idx, float* best_dist,
+                                     float* second_dist, int32_t* accepted, int form) {
+  CHECK_ARG(form == PICP_MATCH_FORM_FULL || form == PICP_MATCH_FORM_ACCEPT_ONLY || form == PICP_MATCH_FORM_EXACT,
+            "picp_match_batch_form: unknown form");
   CHECK_ARG(n_problems >= 1 && n_problems <= 65535 && off1 && off2, "picp_match_batch: bad problem table");
   CHECK_ARG(dim >= 1 && dim <= 32, "picp_match_batch: dim must be in [1, 32]");
   for (int i = 0; i < n_problems; ++i)
@@ -1510,7 +1529,7 @@ extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1,
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)
     e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
-                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, match_accept_only());
+                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form);
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);
@@ -1518,6 +1537,14 @@ extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1,
   hipFree(buf);
   if (e != hipSuccess) return set_err(PICP_ERR_DEVICE, "picp_match_batch: %s", hipGetErrorString(e));
   return PICP_OK;
+}
+
+extern "C" int picp_match_batch(int device, int n_problems, const int64_t* off1, const int64_t* off2,
+                                const float* desc1, const float* desc2, int dim, float dist_thr,
+                                float ratio_thr, int32_t* best_idx, float* best_dist,
+                                float* second_dist, int32_t* accepted) {
+  return picp_match_batch_form(device, n_problems, off1, off2, desc1, desc2, dim, dist_thr, ratio_thr, best_idx,
+                               best_dist, second_dist, accepted, PICP_MATCH_FORM_FULL);
 }
 
 extern "C" int picp_match(int device, const float* desc1, int64_t n1, const float* desc2, int64_t n2,

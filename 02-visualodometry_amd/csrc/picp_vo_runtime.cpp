@@ -28,7 +28,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int accept_only);
+                                             float* second_dist, int32_t* accepted, int form);
 extern "C" int picp_match_prep_kch(int dim);
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
@@ -104,6 +104,7 @@ struct picp_vo {
   // another group's throughput-bound world match.  Group c starts after group c-1's first world
   // match (PICP_VO_PHASE=0: together), so the groups run out of phase.
   int chains = 1;  // PICP_VO_CHAINS (default 1: the serial order)
+  int chains_eff = 1;  // chains for the current segments (1 when two groups would query one frame)
   bool phase = true;
   std::vector<hipStream_t> cstream;  // [chains], [0] unused (the handle's stream)
   std::vector<hipEvent_t> ev_cj;     // [chains]: group c's end (join), [0]: fork
@@ -111,6 +112,9 @@ struct picp_vo {
   int accept_only = 1;  // the sequence reads only accepted matches (PICP_VO_MATCH_FULL=1: full form)
   bool guard = false;
   std::vector<VoGuarded> guards;
+#ifdef PICP_VO_DIAG
+  char* snap = nullptr;  // picp_vo_debug_snap_set: per-step copies of the PICP launch's inputs/outputs
+#endif
 };
 
 
@@ -317,6 +321,29 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     max_steps = std::max(max_steps, (int)G.steps);
     for (int64_t f = G.f0; f < G.f0 + G.steps; ++f) is_curr[f] = 1;
   }
+  // The world match writes its outputs (wm_*) at the query frame's observation offsets.  Two
+  // segments querying one frame at the same step would write the same rows in one launch, so
+  // that layout is rejected; segments querying one frame at different steps are fine in one step
+  // chain (the launches are ordered) but not across chains (PICP_VO_CHAINS=2 runs the groups'
+  // world matches concurrently), so such a layout runs the serial order.
+  int chains_eff = std::min(h->chains, n_seg);
+  {
+    std::vector<int> q_step((size_t)h->n_frames, -1), q_group((size_t)h->n_frames, -1);
+    const int C = chains_eff;
+    for (int s = 0; s < n_seg; ++s) {
+      int grp = 0;
+      while (grp + 1 < C && s >= (int)((int64_t)n_seg * (grp + 1) / C)) ++grp;
+      for (int t = 0; t < steps[s]; ++t) {
+        const int64_t f = first[s] + t + 1;
+        if (q_step[f] == t)
+          return picp_set_err(PICP_ERR_ARG, "picp_vo_set_segments: two segments query frame %lld at step %d",
+                              (long long)f, t);
+        if (q_group[f] >= 0 && q_group[f] != grp) chains_eff = 1;
+        q_step[f] = t;
+        q_group[f] = grp;
+      }
+    }
+  }
   // frame->next problems grouped by step index: chunk k holds frame f0+k of every segment with
   // more than k steps (the bootstrap and step 0 read chunk 0, step t reads chunk t).  Frames of
   // overlapping segments are matched once, in the first chunk that needs them.
@@ -367,6 +394,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   h->ev_chunk.assign((size_t)max_steps, nullptr);
   for (auto& e : h->ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   h->chunk_off = chunk_off;
+  h->chains_eff = chains_eff;
   h->segs = segs;
   h->pprobs = pprobs;
   h->n_seg = n_seg;
@@ -453,17 +481,70 @@ static hipError_t vo_frame_match(picp_vo* h, hipStream_t st, size_t p0, size_t p
   return e;
 }
 
+#ifdef PICP_VO_DIAG
+// Diagnostic build only (tools/vo_snap.py): after step t's PICP launch over segments [s0, s1),
+// copy its problems, initial and final states and SoA planes into snapshot t (layout:
+// picp_vo_debug_snap_bytes).  Copies run on the launch's stream, so they see exactly the block
+// kernel's inputs and outputs.
+static size_t vo_snap_step_bytes(const picp_vo* h) {
+  return (size_t)h->n_seg * (sizeof(PicpProblem) + 2 * sizeof(PicpState) + 5 * (size_t)h->cap_c * sizeof(float));
+}
+static hipError_t vo_snap(picp_vo* h, hipStream_t st, int t, int s0, int s1) {
+  if (!h->snap) return hipSuccess;
+  const VoArgs& V = h->vargs;
+  char* d = h->snap + (size_t)t * vo_snap_step_bytes(h);
+  const size_t ns = (size_t)h->n_seg, k = (size_t)(s1 - s0);
+  hipError_t e = hipMemcpyAsync(d + s0 * sizeof(PicpProblem), V.probs + s0, k * sizeof(PicpProblem),
+                                hipMemcpyDeviceToDevice, st);
+  d += ns * sizeof(PicpProblem);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d + s0 * sizeof(PicpState), V.st_in + s0, k * sizeof(PicpState), hipMemcpyDeviceToDevice, st);
+  d += ns * sizeof(PicpState);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d + s0 * sizeof(PicpState), V.st_out + s0, k * sizeof(PicpState), hipMemcpyDeviceToDevice, st);
+  d += ns * sizeof(PicpState);
+  const float* planes[5] = {V.X, V.Y, V.Z, V.U, V.V};
+  for (int q = 0; q < 5 && e == hipSuccess; ++q)
+    e = hipMemcpyAsync(d + ((size_t)q * ns + s0) * h->cap_c * sizeof(float), planes[q] + (size_t)s0 * h->cap_c,
+                       k * h->cap_c * sizeof(float), hipMemcpyDeviceToDevice, st);
+  return e;
+}
+extern "C" int picp_vo_debug_snap_bytes(picp_vo_t* h, int64_t* per_step, int* n_steps) {
+  CHECK_ARG(h && per_step && n_steps && h->n_seg > 0, "picp_vo_debug_snap_bytes: bad argument");
+  *per_step = (int64_t)vo_snap_step_bytes(h);
+  *n_steps = h->max_steps;
+  return PICP_OK;
+}
+extern "C" int picp_vo_debug_snap_set(picp_vo_t* h, void* dev_buf) {
+  CHECK_ARG(h, "picp_vo_debug_snap_set: bad argument");
+  h->snap = (char*)dev_buf;
+  if (h->exec) {  // re-capture with (or without) the copies
+    hipGraphExecDestroy(h->exec);
+    h->exec = nullptr;
+  }
+  if (h->graph) {
+    hipGraphDestroy(h->graph);
+    h->graph = nullptr;
+  }
+  return PICP_OK;
+}
+#endif
+
 // the whole sequence on the handle's stream.  With overlap on, the frame->next match chunks
 // 1.. run on the side stream (forked after chunk 0, joined by each step's append, which waits
 // for its own chunk): the step chain is a string of latency-bound one-block-per-segment
 // kernels, and the throughput-bound match chunks fill the CUs it leaves idle.
 static hipError_t vo_enqueue(picp_vo* h) {
-  // diagnostic only (wrong results): PICP_VO_DIAG_SKIP bit 1 gather, 2 append, 4 PICP, 8 world
-  // match launches left out of the sequence
+#ifdef PICP_VO_DIAG
+  // diagnostic build only (wrong results; never the shipped library): PICP_VO_DIAG_SKIP bit 1
+  // gather, 2 append, 4 PICP, 8 world match launches left out of the sequence
   static const int skip = [] {
     const char* e = getenv("PICP_VO_DIAG_SKIP");
     return e ? atoi(e) : 0;
   }();
+#else
+  constexpr int skip = 0;
+#endif
   const size_t nck = h->chunk_off.size() - 1;
   const bool ov = h->overlap && nck > 1;
   hipError_t e = vo_frame_match(h, h->stream, 0, ov ? h->chunk_off[1] : h->chunk_off[nck]);
@@ -476,7 +557,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
     }
   }
   if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
-  const int C = std::min(h->chains, h->n_seg);
+  const int C = std::min(h->chains_eff, h->n_seg);
   if (e == hipSuccess && C > 1) e = hipEventRecord(h->ev_cj[0], h->stream);  // fork
   for (int c = 0; c < C && e == hipSuccess; ++c) {
     hipStream_t st = (c == 0) ? h->stream : h->cstream[c];
@@ -498,6 +579,9 @@ static hipError_t vo_enqueue(picp_vo* h) {
         e = picp_launch_block(st, V.n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs + s0,
                               V.st_in + s0, (PicpState*)V.st_out + s0, (int)h->max_obs, 1, nullptr, nullptr,
                               nullptr, 0);
+#ifdef PICP_VO_DIAG
+      if (e == hipSuccess) e = vo_snap(h, st, t, s0, s1);
+#endif
       if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
       if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
     }

@@ -41,11 +41,11 @@ EXPORTED = [
     "picp_batch_get_poses", "picp_batch_get_stats", "picp_batch_solve",
     "picp_batch_solve_async", "picp_batch_sync", "picp_batch_time", "picp_batch_time_single",
     "picp_batch_info", "picp_batch_residency",
-    "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch",
+    "picp_triangulate", "picp_projection_matrix", "picp_match", "picp_match_batch", "picp_match_batch_form",
     "picp_vo_create", "picp_vo_destroy", "picp_vo_set_segments", "picp_vo_run", "picp_vo_run_async", "picp_vo_debug_matches", "picp_vo_debug_guard",
     "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
     "picp_vo_info", "picp_selftest_rcp", "picp_essential_params_default", "picp_essential_batch",
-    "picp_shard_range", "picp_comm_unique_id", "picp_comm_create", "picp_comm_destroy", "picp_comm_info",
+    "picp_shard_range", "picp_shard_pad", "picp_shard_unpack", "picp_comm_unique_id", "picp_comm_create", "picp_comm_destroy", "picp_comm_info",
     "picp_comm_allreduce_max", "picp_comm_barrier", "picp_batch_allgather",
 ]
 COMM_ID_BYTES = 128
@@ -136,6 +136,8 @@ def lib():
                         ctypes.POINTER(ctypes.c_int32)], i),
         "picp_match_batch": ([i, i, ctypes.POINTER(i64), ctypes.POINTER(i64), fp, fp, i, f, f,
                               ctypes.POINTER(ctypes.c_int32), fp, fp, ctypes.POINTER(ctypes.c_int32)], i),
+        "picp_match_batch_form": ([i, i, ctypes.POINTER(i64), ctypes.POINTER(i64), fp, fp, i, f, f,
+                                   ctypes.POINTER(ctypes.c_int32), fp, fp, ctypes.POINTER(ctypes.c_int32), i], i),
         "picp_vo_create": ([ctypes.POINTER(vp), i, i, i, fp, i64, ctypes.POINTER(i64), fp, fp, i], i),
         "picp_vo_destroy": ([vp], i),
         "picp_vo_set_segments": ([vp, i, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_int32), fp, pp], i),
@@ -151,6 +153,8 @@ def lib():
         "picp_selftest_rcp": ([i, i, i, ctypes.POINTER(ctypes.c_uint64)], i),
         "picp_vo_info": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i)], i),
         "picp_shard_range": ([i64, i, i, ctypes.POINTER(i64), ctypes.POINTER(i64)], i),
+        "picp_shard_pad": ([i64, i], i64),
+        "picp_shard_unpack": ([i64, i, i64, vp, vp], i),
         "picp_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], i),
         "picp_comm_create": ([ctypes.POINTER(vp), i, i, i, ctypes.POINTER(ctypes.c_uint8)], i),
         "picp_comm_destroy": ([vp], i),
@@ -397,6 +401,27 @@ def shard_range(n_items, world, rank):
     return a.value, e.value
 
 
+def shard_pad(n_items, world):
+    """picp_shard_pad: rows per rank in the padded all-gather (ceil(n_items / world))."""
+    r = lib().picp_shard_pad(n_items, world)
+    if r < 0:
+        raise PicpError(ERR_ARG, "picp_shard_pad: bad size")
+    return int(r)
+
+
+def shard_unpack(padded, n_items, world):
+    """picp_shard_unpack: the (world * pad, ...) rank-ordered padded rows -> (n_items, ...) in
+    problem order (host code: no device needed)."""
+    padded = np.ascontiguousarray(padded)
+    pad = shard_pad(n_items, world)
+    assert padded.shape[0] == world * max(pad, 1) or (n_items == 0), "padded buffer has the wrong row count"
+    row = padded.dtype.itemsize * int(np.prod(padded.shape[1:], dtype=np.int64))
+    out = np.empty((n_items,) + padded.shape[1:], padded.dtype)
+    _check(lib().picp_shard_unpack(n_items, world, row, padded.ctypes.data_as(ctypes.c_void_p),
+                                   out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
 def comm_unique_id():
     """RCCL unique id (bytes) for Comm; rank 0 makes it, the launcher passes it to every rank."""
     buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
@@ -460,24 +485,22 @@ def _i32ptr(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
 
 
-def match_points(desc1, desc2, dist_thr=0.2, ratio_thr=0.8, device=0):
+# picp_match_batch_form kernel forms (include/picp_c.h PICP_MATCH_FORM_*)
+MATCH_FORMS = {"full": 0, "accept_only": 1, "exact": 2}
+
+
+def match_points(desc1, desc2, dist_thr=0.2, ratio_thr=0.8, device=0, form="full"):
     """match_points (src/my_utilities.h:70-120) on the GPU -> dict(best_idx, best_dist,
-    second_dist, accepted); the reference's correspondences are the accepted (i, best_idx[i])."""
-    d1 = np.ascontiguousarray(desc1, np.float32)
-    d2 = np.ascontiguousarray(desc2, np.float32)
-    n1 = d1.shape[0]
+    second_dist, accepted); the reference's correspondences are the accepted (i, best_idx[i]).
+    form: "full" (default), "accept_only" (only accepted and the best index of accepted queries
+    are defined: the form the VO sequence runs) or "exact" (the exact scan; the same bits)."""
+    d1 = np.asarray(desc1, np.float32)
+    d2 = np.asarray(desc2, np.float32)
     dim = d1.shape[1] if d1.ndim == 2 and d1.shape[1] else (d2.shape[1] if d2.ndim == 2 else 10)
-    n2 = d2.shape[0] if d2.size else 0
-    bi = np.zeros(n1, np.int32)
-    bd = np.zeros(n1, np.float32)
-    sd = np.zeros(n1, np.float32)
-    acc = np.zeros(n1, np.int32)
-    _check(lib().picp_match(device, _fptr(d1), n1, _fptr(d2) if n2 else None, n2, dim, dist_thr, ratio_thr,
-                            _i32ptr(bi), _fptr(bd), _fptr(sd), _i32ptr(acc)))
-    return {"best_idx": bi, "best_dist": bd, "second_dist": sd, "accepted": acc.astype(bool)}
+    return match_points_batch([d1.reshape(-1, dim)], [d2.reshape(-1, dim)], dist_thr, ratio_thr, device, form)[0]
 
 
-def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, device=0):
+def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, device=0, form="full"):
     """Many (set 1, set 2) pairs in one launch; returns a list of per-problem dicts."""
     o1 = np.zeros(len(desc1_list) + 1, np.int64)
     o2 = np.zeros(len(desc2_list) + 1, np.int64)
@@ -491,10 +514,13 @@ def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, devi
     bd = np.zeros(n1, np.float32)
     sd = np.zeros(n1, np.float32)
     acc = np.zeros(n1, np.int32)
-    _check(lib().picp_match_batch(device, len(desc1_list), o1.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-                                  o2.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _fptr(d1),
-                                  _fptr(d2) if d2.size else None, dim, dist_thr, ratio_thr,
-                                  _i32ptr(bi), _fptr(bd), _fptr(sd), _i32ptr(acc)))
+    if n1 == 0:
+        return [{"best_idx": bi, "best_dist": bd, "second_dist": sd, "accepted": acc.astype(bool)}
+                for _ in desc1_list]
+    _check(lib().picp_match_batch_form(device, len(desc1_list), o1.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                       o2.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _fptr(d1),
+                                       _fptr(d2) if d2.size else None, dim, dist_thr, ratio_thr,
+                                       _i32ptr(bi), _fptr(bd), _fptr(sd), _i32ptr(acc), MATCH_FORMS[form]))
     return [{"best_idx": bi[o1[i]:o1[i + 1]], "best_dist": bd[o1[i]:o1[i + 1]],
              "second_dist": sd[o1[i]:o1[i + 1]], "accepted": acc[o1[i]:o1[i + 1]].astype(bool)}
             for i in range(len(desc1_list))]

@@ -588,9 +588,19 @@ def plan_only(args, rk):
             "c4_frames": [f0, f1], "c4_checksum": float(np.float64(bt["xyz"]).sum() + np.float64(bt["uv"]).sum()),
             "c5_segments": list(shard_range(len(first), rk.world, rk.rank))}
     allm = rk.gather_obj(mine)
+    # the C4 results gather in the layout picp_batch_allgather moves over RCCL (padded shards,
+    # picp_shard_unpack): here each rank's initial poses stand in for its solved poses
+    gather_ok = None
+    if rk.dist is not None:
+        from picp_amd.dist import gather_rows
+        rows = bt["T_init"].reshape(f1 - f0, 16)
+        allrows = gather_rows(rows, total, rk.dist)
+        full = synth.make_batch(total, n, base_seed=1000)["T_init"].reshape(total, 16)
+        gather_ok = bool(np.array_equal(allrows, full))
     if rk.rank == 0:
         print(json.dumps({"plan_only": True, "n_gpus": args.gpus, "world_size_observed": rk.world,
-                          "backend": "gloo" if rk.dist is not None else "none", "ranks": allm}), flush=True)
+                          "backend": "gloo" if rk.dist is not None else "none", "ranks": allm,
+                          "c4_gather_matches_single_process": gather_ok}), flush=True)
 
 
 def cpu_baseline_vo(seq, L, budget_s):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PICP_ABI_VERSION 2
+#define PICP_ABI_VERSION 3
 
 /* status codes */
 #define PICP_OK 0
@@ -175,6 +175,13 @@ typedef struct picp_comm picp_comm_t;
 /* Contiguous balanced split of n_items over world ranks: rank owns [*first, *last); sizes differ
  * by at most one (lower ranks take the remainder). */
 int picp_shard_range(int64_t n_items, int world, int rank, int64_t* first, int64_t* last);
+/* The layout picp_batch_allgather moves: every rank contributes its shard padded to
+ * picp_shard_pad(n_items, world) = ceil(n_items / world) items, the all-gather concatenates them
+ * in rank order, and picp_shard_unpack turns that padded buffer (world * pad items of item_bytes
+ * each) back into the n_items items in problem order (rank r's items at picp_shard_range's
+ * [first, last)).  Host memory, no device: the CPU tests drive it for ragged shards. */
+int64_t picp_shard_pad(int64_t n_items, int world);
+int picp_shard_unpack(int64_t n_items, int world, int64_t item_bytes, const void* padded, void* out);
 int picp_comm_unique_id(uint8_t id[PICP_COMM_ID_BYTES]);
 /* Collective over the world: blocks until every rank has joined. */
 int picp_comm_create(picp_comm_t** out, int device, int world, int rank,
@@ -188,7 +195,10 @@ int picp_comm_barrier(picp_comm_t* c);
 /* After a solve of this rank's batch (which must hold exactly picp_shard_range(n_total, world,
  * rank)'s problems): completes it, then all-gathers every rank's per-problem results so that
  * T_all[16 * n_total] (column-major camera poses, problem order) and st_all[n_total] (nullable)
- * hold all of them on every rank.  Collective: every rank calls it. */
+ * hold all of them on every rank.  Collective: every rank calls it.  Every rank's local checks
+ * (shard size, the solve's completion, the staging buffer) are agreed on by one max-allreduce
+ * BEFORE the all-gather, so a rank that fails makes every rank return an error instead of
+ * leaving the others blocked in the collective. */
 int picp_batch_allgather(picp_batch_t* b, picp_comm_t* c, int64_t n_total, float* T_all,
                          picp_stats* st_all);
 
@@ -218,6 +228,18 @@ int picp_match_batch(int device, int n_problems, const int64_t* off1, const int6
                      const float* desc1, const float* desc2, int dim, float dist_thr,
                      float ratio_thr, int32_t* best_idx, float* best_dist, float* second_dist,
                      int32_t* accepted);
+/* picp_match_batch in an explicit kernel form:
+ *   PICP_MATCH_FORM_FULL        the default (MFMA pre-filter + exact rescan; every output);
+ *   PICP_MATCH_FORM_ACCEPT_ONLY the radius form the VO sequence runs: only accepted[] and
+ *                               best_idx of accepted queries are defined (the others are not);
+ *   PICP_MATCH_FORM_EXACT       the exact full scan (the same bits as FULL; a check path). */
+#define PICP_MATCH_FORM_FULL 0
+#define PICP_MATCH_FORM_ACCEPT_ONLY 1
+#define PICP_MATCH_FORM_EXACT 2
+int picp_match_batch_form(int device, int n_problems, const int64_t* off1, const int64_t* off2,
+                          const float* desc1, const float* desc2, int dim, float dist_thr,
+                          float ratio_thr, int32_t* best_idx, float* best_dist, float* second_dist,
+                          int32_t* accepted, int form);
 
 /* ---------------- essential-matrix bootstrap (src/cam.cpp:37-91) ---------------- */
 

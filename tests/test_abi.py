@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     import picp_amd
-    assert picp_amd.lib().picp_abi_version() == 2
+    assert picp_amd.lib().picp_abi_version() == 3  # 3: picp_match_batch_form, picp_shard_pad/unpack
     p = picp_amd.default_params()
     assert (p.threshold, p.damping, p.min_inliers, p.keep_outliers, p.max_rounds) == (1000.0, 1.0, 0, 0, 50)
     assert abs(p.conv_eps - 1e-5) < 1e-12

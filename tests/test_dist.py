@@ -2,7 +2,9 @@
 
 Each rank solves its shard of independent synthetic frames (with the CPU oracle standing in
 for the device solve: this test covers the split/gather plumbing, the GPU tests cover the
-solve), the poses are all-gathered, and rank 0 checks them against a single-process run.
+solve), the poses are all-gathered in picp_batch_allgather's layout (shards padded to
+picp_shard_pad rows, unpacked by the library's picp_shard_unpack), and rank 0 checks them
+against a single-process run.
 """
 import os
 import socket
@@ -22,6 +24,25 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_range(4, 2, 2)
+
+
+def test_shard_pad_unpack_ragged_matches_shard_order():
+    """picp_shard_pad / picp_shard_unpack (the host half of picp_batch_allgather, no device):
+    ragged shards padded to ceil(n / world) rows and concatenated in rank order come back in
+    problem order, bit-exact; picp_shard_range agrees with the Python split."""
+    import picp_amd
+    from picp_amd.dist import shard_range
+    for n, w in ((1025, 8), (9, 2), (5, 8), (0, 3), (7, 1), (128, 3)):
+        pad = max(picp_amd.shard_pad(n, w), 1)
+        full = np.arange(n * 32, dtype=np.int32).reshape(n, 32)  # a 128-byte PicpState per row
+        padded = np.full((w * pad, 32), -1, np.int32)
+        for r in range(w):
+            a, e = shard_range(n, w, r)
+            assert picp_amd.shard_range(n, w, r) == (a, e)
+            padded[r * pad:r * pad + e - a] = full[a:e]
+        np.testing.assert_array_equal(picp_amd.shard_unpack(padded, n, w), full)
+    with pytest.raises(picp_amd.PicpError):
+        picp_amd.shard_pad(4, 0)
 
 
 def _free_port():
@@ -96,6 +117,7 @@ def test_bench_launcher_gpus2_plan_only_starts_shards_and_gathers():
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["plan_only"] and out["n_gpus"] == 2 and out["world_size_observed"] == 2
+    assert out["c4_gather_matches_single_process"] is True  # 9 frames over 2 ranks: padded 5 + 4
     ranks = out["ranks"]
     assert [x["rank"] for x in ranks] == [0, 1] and ranks[0]["pid"] != ranks[1]["pid"]
     assert [x["c4_frames"] for x in ranks] == [[0, 5], [5, 9]]

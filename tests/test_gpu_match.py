@@ -12,18 +12,26 @@ _MODE = {"kernel": "mfma"}
 
 @pytest.fixture(params=["mfma", "exact", "accept_only"], autouse=True)
 def matcher_kernel(request, monkeypatch):
-    """Every test runs on three forms: the MFMA pre-filter (default) and the exact scan
-    (PICP_MATCH_EXACT=1, read at each launch) must give the oracle's bits; the accept-only
-    radius form the VO sequence runs (PICP_MATCH_ACCEPT_ONLY=1) must give the oracle's accept
-    flags, and its best index and best distance wherever a query is accepted."""
-    for k in ("PICP_MATCH_EXACT", "PICP_MATCH_ACCEPT_ONLY"):
-        monkeypatch.delenv(k, raising=False)
-    if request.param == "exact":
-        monkeypatch.setenv("PICP_MATCH_EXACT", "1")
-    elif request.param == "accept_only":
-        monkeypatch.setenv("PICP_MATCH_ACCEPT_ONLY", "1")
+    """Every test runs on three forms, selected by picp_match_batch_form's explicit argument: the
+    MFMA pre-filter (the default "full" form) and the exact scan ("exact") must give the oracle's
+    bits; the accept-only radius form the VO sequence runs ("accept_only") must give the oracle's
+    accept flags, and its best index and best distance wherever a query is accepted."""
+    import functools
+
+    import picp_amd
+    form = {"mfma": "full", "exact": "exact", "accept_only": "accept_only"}[request.param]
+    monkeypatch.setattr(picp_amd, "match_points", functools.partial(_MATCH[0], form=form))
+    monkeypatch.setattr(picp_amd, "match_points_batch", functools.partial(_MATCH[1], form=form))
     _MODE["kernel"] = request.param
     return request.param
+
+
+def _unpatched():
+    import picp_amd
+    return picp_amd.match_points, picp_amd.match_points_batch
+
+
+_MATCH = _unpatched()
 
 
 def _eq(got, ref):

@@ -33,9 +33,12 @@ for rep in range(2):
         for kv in v.split(","):
             k, val = kv.split("=")
             os.environ[k] = val
-        picp_amd.match_points_batch(d1s, d2s)
+        # PICP_MATCH_ACCEPT_ONLY / PICP_MATCH_EXACT name the explicit form argument
+        form = "exact" if os.environ.get("PICP_MATCH_EXACT") == "1" else (
+            "accept_only" if os.environ.get("PICP_MATCH_ACCEPT_ONLY") == "1" else "full")
+        picp_amd.match_points_batch(d1s, d2s, form=form)
         t = time.perf_counter()
-        out = picp_amd.match_points_batch(d1s, d2s)
+        out = picp_amd.match_points_batch(d1s, d2s, form=form)
         print(v, "%.2f ms (incl. copies)" % (1e3 * (time.perf_counter() - t)), sum(int(o["accepted"].sum()) for o in out))
         for kv in v.split(","):
             os.environ.pop(kv.split("=")[0], None)

@@ -20,7 +20,10 @@ d2 = [desc[off[f + 1]:off[f + 2]] for f in range(F - 1)]
 def run(env):
     for k, v in env.items():
         os.environ[k] = v
-    r = picp_amd.match_points_batch(d1, d2)
+    # the kernel form is an explicit argument (picp_match_batch_form); the two keys name it
+    form = "exact" if env.get("PICP_MATCH_EXACT") == "1" else (
+        "accept_only" if env.get("PICP_MATCH_ACCEPT_ONLY") == "1" else "full")
+    r = picp_amd.match_points_batch(d1, d2, form=form)
     for k in env:
         del os.environ[k]
     acc = np.concatenate([x["accepted"] for x in r])
