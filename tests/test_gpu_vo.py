@@ -133,8 +133,8 @@ def test_vo_synthetic_segments(native, oracle, n_frames, obs, seg_len, noise):
 
 def test_vo_replay_and_segment_independence(native, monkeypatch):
     """Replays are bit-identical, and a segment's result does not depend on which other segments
-    run beside it (one block per segment, no cross-segment state).  Pinned to the serial order
-    (the default; the opt-in concurrent schedule is not bit-stable)."""
+    run beside it (one block per segment, no cross-segment state).  Pinned to the serial order;
+    test_vo_step_schedules_bit_identical covers the concurrent ones."""
     for k, v in {"PICP_VO_CHAINS": "1", "PICP_VO_OVERLAP": "0"}.items():
         monkeypatch.setenv(k, v)
     from picp_amd.vo_synth import VOSequence
@@ -160,9 +160,8 @@ def test_vo_replay_and_segment_independence(native, monkeypatch):
 
 
 def test_vo_graph_and_direct_enqueue_identical(native, monkeypatch):
-    """The default serial order replayed from its hipGraph and enqueued launch by launch
-    (PICP_VO_GRAPH=0) give bit-identical poses, step records and maps, run after run.  (The
-    opt-in concurrent schedule, PICP_VO_OVERLAP=1 / PICP_VO_CHAINS=2, does not: DESIGN.md §4.9.)"""
+    """The serial order replayed from its hipGraph and enqueued launch by launch (PICP_VO_GRAPH=0)
+    give bit-identical poses, step records and maps, run after run."""
     from picp_amd.vo_synth import VOSequence, segments
     s = VOSequence(1201, obs_per_frame=1200, seed=5)
     F = s.frames(0, 1201)
@@ -178,6 +177,8 @@ def test_vo_graph_and_direct_enqueue_identical(native, monkeypatch):
         seq.close()
         return out
 
+    monkeypatch.setenv("PICP_VO_OVERLAP", "0")
+    monkeypatch.setenv("PICP_VO_CHAINS", "1")
     base = run()
     monkeypatch.setenv("PICP_VO_GRAPH", "0")
     other = run()
@@ -206,3 +207,104 @@ def test_vo_argument_errors(native):
     seq.set_segments([0], [5], boot)
     seq.run()
     assert seq.step_records()[0]["n_corr"][1:].min() > 0
+
+
+def _vo_outputs(native, F, K, first, steps, boot, runs=2):
+    seq = native.VOSequence(F["frame_off"], F["uv"], F["desc"], K=K)
+    seq.set_segments(first, steps, boot, threshold=THR)
+    outs = []
+    for _ in range(runs):
+        seq.run()
+        outs.append((seq.poses(), seq.step_records(), [seq.map(k) for k in range(len(first))]))
+    seq.close()
+    return outs
+
+
+def _assert_same_bits(a, b, what):
+    for x, y in zip(a[0], b[0]):
+        np.testing.assert_array_equal(np.asarray(x).view(np.uint32), np.asarray(y).view(np.uint32), err_msg=what)
+    for x, y in zip(a[1], b[1]):
+        for f in ("n_corr", "n_in", "rounds", "n_new", "chi_in"):
+            np.testing.assert_array_equal(np.asarray(x[f]), np.asarray(y[f]), err_msg=what + " " + f)
+    for (xa, da), (xb, db) in zip(a[2], b[2]):
+        np.testing.assert_array_equal(xa.view(np.uint32), xb.view(np.uint32), err_msg=what + " map")
+        np.testing.assert_array_equal(da, db, err_msg=what + " map descriptors")
+
+
+def test_vo_step_schedules_bit_identical(native, monkeypatch):
+    """The concurrent step schedules -- the frame->next match beside the step chain
+    (PICP_VO_OVERLAP=1), two step chains (PICP_VO_CHAINS=2), both -- give the serial order's
+    poses, step records and maps bit for bit, run after run.  Before the kernels were built
+    without packed FP32 (picp_internal.h PICP_KERNEL_FP32), the matcher's MFMA waves beside the
+    PICP block kernel changed its lanes 48-63 and this differed in every run."""
+    from picp_amd.vo_synth import VOSequence, segments
+    s = VOSequence(2001, obs_per_frame=2000, seed=42)
+    F = s.frames(0, 2001)
+    first, steps = segments(2001, 40)
+    rel = [np.linalg.inv(F["T_cw"][f].astype(np.float64)) for f in first]
+    boot = np.stack([[np.eye(4), rel[k] @ F["T_cw"][f + 1]] for k, f in enumerate(first)]).astype(np.float32)
+    schedules = [{"PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"}, {"PICP_VO_OVERLAP": "1", "PICP_VO_CHAINS": "1"},
+                 {"PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "2"}, {"PICP_VO_OVERLAP": "1", "PICP_VO_CHAINS": "2"}]
+    ref = None
+    for env in schedules:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        outs = _vo_outputs(native, F, s.K, first, steps, boot)
+        if ref is None:
+            ref = outs[0]
+        for o in outs:
+            _assert_same_bits(ref, o, str(env))
+
+
+def test_block_batch_beside_vo_bit_identical(native, monkeypatch):
+    """A block-mode batch (the C4/C5 kernel) solved on its own stream while a VO sequence runs
+    its matcher (MFMA) and step kernels beside it gives the bits of its solo run, every rep."""
+    from picp_amd import synth
+    from picp_amd.vo_synth import VOSequence, segments
+    monkeypatch.setenv("PICP_MODE", "block")
+    monkeypatch.setenv("PICP_VO_OVERLAP", "1")
+    bt = synth.make_batch(250, 1500, base_seed=1000)
+    B = native.Batch(np.full(250, 1500))
+    B.set_data(bt["xyz"], bt["uv"])
+    assert B.info()["mode"] == "block"
+    B.set_poses(bt["T_init"])
+    B.solve(max_rounds=50, conv_eps=1e-5)
+    ref = B.poses().copy()
+    s = VOSequence(1201, obs_per_frame=1200, seed=9)
+    F = s.frames(0, 1201)
+    first, steps = segments(1201, 40)
+    boot = np.stack([[F["T_cw"][f], F["T_cw"][f + 1]] for f in first])
+    vo = native.VOSequence(F["frame_off"], F["uv"], F["desc"], K=s.K)
+    vo.set_segments(first, steps, boot, threshold=THR)
+    L = native.lib()
+    for _ in range(6):
+        B.set_poses(bt["T_init"])
+        assert L.picp_vo_run_async(vo._h) == 0
+        B.solve_async(max_rounds=50, conv_eps=1e-5)
+        B.sync()
+        assert L.picp_vo_sync(vo._h) == 0
+        np.testing.assert_array_equal(B.poses().view(np.uint32), ref.view(np.uint32))
+    vo.close()
+    B.close()
+
+
+def test_vo_segments_querying_one_frame(native, monkeypatch):
+    """Two segments that query one frame at the same step would write the same world-match rows
+    in one launch: rejected.  Segments that query one frame at different steps run; with two step
+    chains whose groups would share that frame the handle runs the serial order, so the result
+    equals the serial handle's bit for bit."""
+    from picp_amd.vo_synth import VOSequence
+    s = VOSequence(14, obs_per_frame=600, seed=4)
+    F = s.frames(0, 14)
+    boot = lambda fs: np.stack([[F["T_cw"][f], F["T_cw"][f + 1]] for f in fs])  # noqa: E731
+    seq = native.VOSequence(F["frame_off"], F["uv"], F["desc"], K=s.K)
+    with pytest.raises(native.PicpError):
+        seq.set_segments([0, 0], [5, 5], boot([0, 0]))
+    seq.close()
+    first, steps = np.array([0, 3]), np.array([8, 8])  # frames 4..9 queried by both, other steps
+    monkeypatch.setenv("PICP_VO_OVERLAP", "0")
+    monkeypatch.setenv("PICP_VO_CHAINS", "1")
+    ref = _vo_outputs(native, F, s.K, first, steps, boot(first), runs=1)[0]
+    monkeypatch.setenv("PICP_VO_CHAINS", "2")
+    got = _vo_outputs(native, F, s.K, first, steps, boot(first), runs=1)[0]
+    _assert_same_bits(ref, got, "chains=2, shared query frames")

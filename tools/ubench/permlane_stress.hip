@@ -24,6 +24,16 @@
 //             chain whose every v_rcp_f32 is followed by 16 wait states (inline asm); mismatches
 //             counted for lanes 0-47 in the low half of the counter and lanes 48-63 times 2^32
 //   victim 8: the same with v_sqrt_f32 / v_rsq_f32 / v_exp_f32 / v_log_f32 producers
+//   victim 9: apply_update (picp_device.h: Rx*Ry*Rz compose, packed-FP32 code) on inputs that are
+//             the same in every lane: every lane must get lane 0's bits (lanes 0-47 / 48-63 counted
+//             as in victim 7); victim 10: the same chain of packed FMAs (v_pk_fma_f32) alone
+//   victims 11-16: one packed-FP32 instruction form each (inline asm, dependent chains, inputs the
+//             same in every lane, lane agreement as victim 9): 11 v_pk_mul_f32 op_sel_hi:[1,0],
+//             12 v_pk_mul_f32 op_sel:[1,1] op_sel_hi:[0,0], 13 v_pk_fma_f32 neg_lo/neg_hi on src2,
+//             14 v_pk_fma_f32 op_sel:[0,0,1] op_sel_hi:[1,1,0], 15 v_pk_add_f32, 16 v_pk_fma_f32 plain
+//   victims 17-22: a 32-bit VALU write of one half of a register pair, then a packed-FP32 read
+//             of the pair after 0 / 1 / 2 wait states (inline asm, explicit v200-v205): 17/18/19
+//             the high half written, 20/21/22 the low half written
 //   aggressors: 0 none, 1 MFMA f16, 2 LDS traffic, 3 victim-0 itself, 4 FP32 FMA, 5 FP64 FMA,
 //               6 DPP moves, 7 ds_bpermute, 8 v_permlane32_swap, 9 f32 transcendentals,
 //               10 f64 transcendentals (v_rcp_f64 / v_sqrt_f64)
@@ -176,6 +186,88 @@ __global__ __launch_bounds__(512) void victim(int iters, unsigned long long* bad
       const unsigned long long d = (__float_as_uint(xf) != __float_as_uint(xr)) ? 1ull : 0ull;
       nb += (lane >= 48) ? (d << 32) : d;
       nc += 64;
+    } else if (VICTIM == 9) {
+      float R[9], t[3], dx[6];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : 1e-3f * (float)((int)(val(w, it, 0, i) & 63) - 32);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) t[i] = 1e-2f * (float)((int)(val(w, it, 0, 9 + i) & 255) - 128);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) dx[i] = 1e-5f * (float)((int)(val(w, it, 0, 12 + i) & 1023) - 512);
+      for (int k = 0; k < 8; ++k) {
+        apply_update(dx, R, t);
+        dx[3] += 1e-7f * R[1];
+      }
+      bool mism = false;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) mism |= __float_as_int(R[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(R[i]));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) mism |= __float_as_int(t[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(t[i]));
+      const unsigned long long d = mism ? 1ull : 0ull;
+      nb += (lane >= 48) ? (d << 32) : d;
+      nc += 8;
+    } else if (VICTIM == 10) {
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      f2v a = {1.0f + 1e-3f * (float)(val(w, it, 0, 0) & 255), 1.0f + 1e-3f * (float)(val(w, it, 0, 1) & 255)};
+      f2v b = {0.999f, 1.001f}, c = {1e-3f, -1e-3f};
+#pragma unroll 8
+      for (int k = 0; k < 256; ++k) {
+        a = __builtin_elementwise_fma(a, b, c);
+        b = __builtin_elementwise_fma(b, a, c) * 0.5f;
+        c = (f2v){c.y, c.x};
+      }
+      const bool mism = (__float_as_int(a.x) != __builtin_amdgcn_readfirstlane(__float_as_int(a.x))) |
+                        (__float_as_int(a.y) != __builtin_amdgcn_readfirstlane(__float_as_int(a.y))) |
+                        (__float_as_int(b.x) != __builtin_amdgcn_readfirstlane(__float_as_int(b.x)));
+      const unsigned long long d = mism ? 1ull : 0ull;
+      nb += (lane >= 48) ? (d << 32) : d;
+      nc += 256;
+    } else if (VICTIM >= 11 && VICTIM <= 16) {
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      f2v a = {1.0f + 1e-3f * (float)(val(w, it, 0, 0) & 255), 1.0f - 1e-3f * (float)(val(w, it, 0, 1) & 255)};
+      f2v b = {0.75f, 1.25f}, c = {1e-3f, -2e-3f}, r;
+#pragma unroll 4
+      for (int k = 0; k < 64; ++k) {
+        if (VICTIM == 11) asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+        else if (VICTIM == 12) asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0]" : "=v"(r) : "v"(a), "v"(b));
+        else if (VICTIM == 13) asm volatile("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[0,0,1] neg_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+        else if (VICTIM == 14) asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+        else if (VICTIM == 15) asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+        else asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+        // renormalise into [0.5, 2) with plain VALU (the next producer's operands written right before it)
+        a = (f2v){r.x * 0.5f + 0.75f, r.y * 0.5f + 0.5f};
+      }
+      const bool mism = (__float_as_int(a.x) != __builtin_amdgcn_readfirstlane(__float_as_int(a.x))) |
+                        (__float_as_int(a.y) != __builtin_amdgcn_readfirstlane(__float_as_int(a.y)));
+      const unsigned long long d = mism ? 1ull : 0ull;
+      nb += (lane >= 48) ? (d << 32) : d;
+      nc += 64;
+    } else if (VICTIM >= 17 && VICTIM <= 22) {
+      float x = 1.0f + 1e-3f * (float)(val(w, it, 0, 0) & 255), y = 1.0f - 1e-3f * (float)(val(w, it, 0, 1) & 255);
+      float rl = 0.0f, rh = 0.0f;
+#define PK_SEQ(WRITE, NOPS)                                                                           \
+  asm volatile("v_mov_b32 v200, %2\n\tv_mov_b32 v201, %3\n\tv_mov_b32 v202, 0x3f400000\n\t"             \
+               "v_mov_b32 v203, 0x3fa00000\n\ts_nop 7\n\t" WRITE NOPS                                    \
+               "v_pk_mul_f32 v[204:205], v[200:201], v[202:203]\n\ts_nop 7\n\t"                          \
+               "v_mov_b32 %0, v204\n\tv_mov_b32 %1, v205"                                                \
+               : "=v"(rl), "=v"(rh) : "v"(x), "v"(y) : "v200", "v201", "v202", "v203", "v204", "v205")
+#pragma unroll 2
+      for (int k = 0; k < 64; ++k) {
+        if (VICTIM == 17) PK_SEQ("v_add_f32 v203, 0x3fa00000, v200\n\t", "");
+        else if (VICTIM == 18) PK_SEQ("v_add_f32 v203, 0x3fa00000, v200\n\t", "s_nop 0\n\t");
+        else if (VICTIM == 19) PK_SEQ("v_add_f32 v203, 0x3fa00000, v200\n\t", "s_nop 1\n\t");
+        else if (VICTIM == 20) PK_SEQ("v_add_f32 v202, 0x3f400000, v201\n\t", "");
+        else if (VICTIM == 21) PK_SEQ("v_add_f32 v202, 0x3f400000, v201\n\t", "s_nop 0\n\t");
+        else PK_SEQ("v_add_f32 v202, 0x3f400000, v201\n\t", "s_nop 1\n\t");
+        x = rl * 0.25f + 0.75f;
+        y = rh * 0.25f + 0.5f;
+      }
+#undef PK_SEQ
+      const bool mism = (__float_as_int(x) != __builtin_amdgcn_readfirstlane(__float_as_int(x))) |
+                        (__float_as_int(y) != __builtin_amdgcn_readfirstlane(__float_as_int(y)));
+      const unsigned long long d = mism ? 1ull : 0ull;
+      nb += (lane >= 48) ? (d << 32) : d;
+      nc += 64;
     } else if (VICTIM == 4) {
       // (the loop below runs the whole test once; `it` stays 0 here)
       unsigned hold[96];
@@ -274,6 +366,43 @@ __global__ __launch_bounds__(512) void victim(int iters, unsigned long long* bad
     }
   }
   // one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    nb += __shfl_xor(nb, o);
+    nc += __shfl_xor(nc, o);
+  }
+  if (lane == 0) {
+    atomicAdd(bad, nb);
+    atomicAdd(checks, nc);
+  }
+}
+
+// victim 23: victim 9 (apply_update, lane agreement) in a kernel compiled without packed FP32
+__global__ __launch_bounds__(512) __attribute__((target("no-packed-fp32-ops"))) void victim_nopk(
+    int iters, unsigned long long* bad, unsigned long long* checks) {
+  const int lane = threadIdx.x & 63;
+  const unsigned w = blockIdx.x * 8 + (threadIdx.x >> 6);
+  unsigned long long nb = 0, nc = 0;
+  for (int it = 0; it < iters; ++it) {
+    float R[9], t[3], dx[6];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : 1e-3f * (float)((int)(val(w, it, 0, i) & 63) - 32);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] = 1e-2f * (float)((int)(val(w, it, 0, 9 + i) & 255) - 128);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dx[i] = 1e-5f * (float)((int)(val(w, it, 0, 12 + i) & 1023) - 512);
+    for (int k = 0; k < 8; ++k) {
+      apply_update(dx, R, t);
+      dx[3] += 1e-7f * R[1];
+    }
+    bool mism = false;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) mism |= __float_as_int(R[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(R[i]));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) mism |= __float_as_int(t[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(t[i]));
+    const unsigned long long d = mism ? 1ull : 0ull;
+    nb += (lane >= 48) ? (d << 32) : d;
+    nc += 8;
+  }
   for (int o = 32; o > 0; o >>= 1) {
     nb += __shfl_xor(nb, o);
     nc += __shfl_xor(nc, o);
@@ -411,6 +540,21 @@ int main(int argc, char** argv) {
   else if (vk == 6) hipLaunchKernelGGL(victim<6>, vg, vb, 0, sv, iters, d, d + 1);
   else if (vk == 7) hipLaunchKernelGGL(victim<7>, vg, vb, 0, sv, iters, d, d + 1);
   else if (vk == 8) hipLaunchKernelGGL(victim<8>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 9) hipLaunchKernelGGL(victim<9>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 10) hipLaunchKernelGGL(victim<10>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 11) hipLaunchKernelGGL(victim<11>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 12) hipLaunchKernelGGL(victim<12>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 13) hipLaunchKernelGGL(victim<13>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 14) hipLaunchKernelGGL(victim<14>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 15) hipLaunchKernelGGL(victim<15>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 16) hipLaunchKernelGGL(victim<16>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 23) hipLaunchKernelGGL(victim_nopk, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 17) hipLaunchKernelGGL(victim<17>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 18) hipLaunchKernelGGL(victim<18>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 19) hipLaunchKernelGGL(victim<19>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 20) hipLaunchKernelGGL(victim<20>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 21) hipLaunchKernelGGL(victim<21>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 22) hipLaunchKernelGGL(victim<22>, vg, vb, 0, sv, iters, d, d + 1);
   else hipLaunchKernelGGL(victim<2>, vg, vb, 0, sv, iters, d, d + 1);
   CK(hipGetLastError());
   CK(hipEventRecord(done, sv));
@@ -423,7 +567,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   unsigned long long h[2];
   CK(hipMemcpy(h, d, 16, hipMemcpyDeviceToHost));
-  if (vk == 7 || vk == 8)
+  if (vk >= 7)
     printf("victim %d aggressor %d: %llu mismatches in lanes 0-47, %llu in lanes 48-63, %llu chain steps (%d aggressor launches)\n",
            vk, ak, h[0] & 0xFFFFFFFFull, h[0] >> 32, h[1], ak ? n_aggr : 0);
   else
@@ -446,6 +590,8 @@ extern "C" int stress_launch(int vk, int blocks, int iters, void* stream, unsign
   else if (vk == 6) hipLaunchKernelGGL(victim<6>, vg, vb, 0, s, iters, d_counts, d_counts + 1);
   else if (vk == 7) hipLaunchKernelGGL(victim<7>, vg, vb, 0, s, iters, d_counts, d_counts + 1);
   else if (vk == 8) hipLaunchKernelGGL(victim<8>, vg, vb, 0, s, iters, d_counts, d_counts + 1);
+  else if (vk == 9) hipLaunchKernelGGL(victim<9>, vg, vb, 0, s, iters, d_counts, d_counts + 1);
+  else if (vk == 10) hipLaunchKernelGGL(victim<10>, vg, vb, 0, s, iters, d_counts, d_counts + 1);
   else hipLaunchKernelGGL(victim<2>, vg, vb, 0, s, iters, d_counts, d_counts + 1);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -60,13 +60,13 @@ def beside(victim, what, iters):
             L.picp_vo_sync(handles[what]._h)
         assert hip.hipStreamSynchronize(st) == 0
     assert hip.hipMemcpy(h.ctypes.data_as(ctypes.c_void_p), cnt, ctypes.c_size_t(16), 2) == 0
-    if victim in (7, 8):
+    if victim in (7, 8, 9, 10):
         print("victim %d beside %-8s: %d mismatches in lanes 0-47, %d in lanes 48-63, %d chain steps"
               % (victim, what, int(h[0]) & 0xFFFFFFFF, int(h[0]) >> 32, int(h[1])), flush=True)
     else:
         print("victim %d beside %-8s: %d mismatches in %d checks" % (victim, what, int(h[0]), int(h[1])), flush=True)
 
 
-for victim, iters in ((7, 400), (8, 400), (3, 2000)):
+for victim, iters in ((9, 1000), (10, 100)):
     for what in ("none", "serial", "overlap", "batch"):
         beside(victim, what, iters)
