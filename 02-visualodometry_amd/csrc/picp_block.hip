@@ -106,7 +106,7 @@ extern "C" hipError_t picp_debug_bdiag_set(float* buf, int n_problems, int round
 #endif
 
 template <int NPT, int PH, int BS>
-__global__ __launch_bounds__(BS, 2) PICP_KERNEL_FP32 void picp_block_kernel(
+__global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,

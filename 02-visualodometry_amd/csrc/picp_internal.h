@@ -71,20 +71,17 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 // ---------------------------------------------------------------------------------------
 // descriptor matching (picp_match.hip): query rows [q_off, q_off + nq) of the query
 // descriptors against reference rows [r_off, r_off + nr); best_idx is relative to r_off.
-// Every PICP kernel is compiled WITHOUT packed-FP32 VALU instructions (v_pk_fma/mul/add_f32).
-// On MI355X (gfx950, ROCm 7.2) the compiler's packed code for apply_update gave lanes 48-63 of a
-// wave results that differ from lanes 0-47 on identical inputs whenever an MFMA kernel ran on the
-// same CU (tools/ubench/permlane_stress.hip victim 9: ~1.5e-4 of the updates beside an MFMA
-// kernel, none alone or beside LDS / FP32 / FP64 / transcendental / DPP / permlane load; the
-// scalar build of the same function, victim 23, none).  In the VO sequence that made the PICP
-// poses depend on whether the matcher ran beside the block kernel.  The scalar
-// code measured as fast or faster (the linearize is issue-bound either way).  -DPICP_ALLOW_PK
-// restores packed code for A/B builds.
-#if defined(PICP_ALLOW_PK)
-#define PICP_KERNEL_FP32
-#else
-#define PICP_KERNEL_FP32 __attribute__((target("no-packed-fp32-ops")))
-#endif
+// Every PICP device translation unit is compiled WITHOUT packed-FP32 VALU instructions
+// (v_pk_fma/mul/add_f32): hipcc_nopk.sh passes -target-feature -packed-fp32-ops to the whole
+// device compile.  On MI355X (gfx950, ROCm 7.2) the compiler's packed code for apply_update gave
+// lanes 48-63 of a wave results that differ from lanes 0-47 on identical inputs whenever an MFMA
+// kernel ran on the same CU (tools/ubench/permlane_stress.hip victim 9 beside an MFMA kernel; none
+// alone or beside LDS / FP32 / FP64 / transcendental / DPP / permlane load; the scalar build of the
+// same function, victim 23, none).  In the VO sequence that made the PICP poses depend on whether
+// the matcher ran beside the block kernel.  The flag is TU-wide on purpose: a
+// per-kernel target("no-packed-fp32-ops") attribute stops HIP's header functions (__syncthreads,
+// ...) from inlining into the kernel, and the calls cost C2 18 % and C5 80 % (round-3 pass).
+// `make PK=1` restores packed code (-DPICP_ALLOW_PK) for A/B builds.
 
 // Diagnostic build only (-DPICP_KFENCE): explicit agent-scope acquire at the start and release at
 // the end of the VO path's kernels, to test whether kernel-boundary visibility is what differs

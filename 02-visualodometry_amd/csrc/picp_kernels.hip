@@ -102,7 +102,7 @@ __device__ __forceinline__ void reduce_published(const unsigned long long* __res
 // over every SIMD).  tickets[p] are zeroed by a memset node before launch 0 and re-zeroed by
 // each last arriver.
 template <int VEC, int PH>
-__global__ __launch_bounds__(PICP_BLOCK) PICP_KERNEL_FP32 void picp_round_kernel(
+__global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const int4* __restrict__ blkinfo,
@@ -315,7 +315,7 @@ extern "C" hipError_t picp_debug_stamps(unsigned long long* out, size_t n_words)
 #endif
 
 // IntPairVector gather: pairs[k] = (image idx, world idx) (src/picp_solver.cpp:65-66).
-extern "C" __global__ PICP_KERNEL_FP32 void picp_gather_kernel(const float* __restrict__ world,
+extern "C" __global__ void picp_gather_kernel(const float* __restrict__ world,
                                               const float* __restrict__ image,
                                               const int2* __restrict__ pairs, int64_t m,
                                               float* __restrict__ X, float* __restrict__ Y,
@@ -335,7 +335,7 @@ extern "C" __global__ PICP_KERNEL_FP32 void picp_gather_kernel(const float* __re
 // convertPointsFromHomogeneous :118).  One lane per point; A (4x4) in double, right singular
 // vector of the smallest singular value by one-sided (Hestenes) Jacobi with a fixed sweep
 // count, all indices compile-time so A and V live in registers.
-extern "C" __global__ PICP_KERNEL_FP32 void picp_triangulate_kernel(const float* __restrict__ P1,
+extern "C" __global__ void picp_triangulate_kernel(const float* __restrict__ P1,
                                                    const float* __restrict__ P2,
                                                    const float2* __restrict__ uv1,
                                                    const float2* __restrict__ uv2, int64_t q,

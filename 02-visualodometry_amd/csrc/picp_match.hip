@@ -45,7 +45,7 @@ __device__ inline void match_update(float d, int32_t j, float& best, float& seco
 }
 
 template <int D>  // D > 0: compile-time dim; D == 0: runtime dim <= PICP_MATCH_MAXD
-__global__ __launch_bounds__(PICP_MATCH_BLOCK) PICP_KERNEL_FP32 void picp_match_kernel(
+__global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const MatchProblem* __restrict__ probs, int dim_rt, float dist_thr, float ratio_thr,
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
@@ -186,7 +186,7 @@ __device__ __forceinline__ void mm_split(float x, _Float16& hi, _Float16& lo) {
 //   n1 = |x|^2, +inf if a component is non-finite or beyond +-60000 (fp16 range): pass 1
 //   n2 = |x|^2, -inf for such a row: pass 2 (an unsafe reference is every query's candidate)
 // An unsafe row's fp16 values are zeroed so its MFMA products stay finite.
-extern "C" __global__ PICP_KERNEL_FP32 void picp_match_prep_kernel(const float* __restrict__ desc, int64_t n, int dim,
+extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc, int64_t n, int dim,
                                                   int kch, _Float16* __restrict__ h,
                                                   float* __restrict__ n1, float* __restrict__ n2) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -308,7 +308,7 @@ __device__ __forceinline__ unsigned mm_mask16_ge0(const mm_f16v& acc) {
 #define MM_MINB 1
 #endif
 template <int KCH, int RAD, int RB>
-__global__ __launch_bounds__(MM_BLOCK, MM_MINB) PICP_KERNEL_FP32 void picp_match_mfma_kernel(
+__global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
     const _Float16* __restrict__ r_h, const float* __restrict__ r_n1, const float* __restrict__ r_n2,

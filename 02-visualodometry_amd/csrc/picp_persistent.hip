@@ -66,7 +66,7 @@ __device__ __forceinline__ bool timed_out(unsigned long long deadline) {
 }
 
 template <int NPT, int PH>
-__global__ __launch_bounds__(PICP_PBLOCK) PICP_KERNEL_FP32 void picp_persistent_kernel(
+__global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,

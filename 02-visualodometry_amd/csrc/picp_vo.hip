@@ -96,7 +96,7 @@ __device__ inline int vo_block_rank(bool flag, int* s_cnt, int* total) {
   return pre + r;
 }
 
-__global__ __launch_bounds__(VO_BLOCK) PICP_KERNEL_FP32 void vo_gather_kernel(const VoArgs a, int t) {
+__global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int t) {
   PICP_KFENCE_IN();
   const int s = a.seg0 + (int)blockIdx.x;
   const VoSegment G = a.segs[s];
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(VO_BLOCK) PICP_KERNEL_FP32 void vo_gather_kernel(co
   PICP_KFENCE_OUT();
 }
 
-__global__ __launch_bounds__(VOA_BLOCK) PICP_KERNEL_FP32 void vo_append_kernel(const VoArgs a, int t) {
+__global__ __launch_bounds__(VOA_BLOCK) void vo_append_kernel(const VoArgs a, int t) {
   PICP_KFENCE_IN();
   const int s = a.seg0 + (int)blockIdx.x;
   const VoSegment G = a.segs[s];

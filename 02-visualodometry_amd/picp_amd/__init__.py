@@ -497,7 +497,7 @@ def match_points(desc1, desc2, dist_thr=0.2, ratio_thr=0.8, device=0, form="full
     d1 = np.asarray(desc1, np.float32)
     d2 = np.asarray(desc2, np.float32)
     dim = d1.shape[1] if d1.ndim == 2 and d1.shape[1] else (d2.shape[1] if d2.ndim == 2 else 10)
-    return match_points_batch([d1.reshape(-1, dim)], [d2.reshape(-1, dim)], dist_thr, ratio_thr, device, form)[0]
+    return match_points_batch([d1.reshape(-1, dim)], [d2.reshape(-1, dim)], dist_thr, ratio_thr, device, form=form)[0]
 
 
 def match_points_batch(desc1_list, desc2_list, dist_thr=0.2, ratio_thr=0.8, device=0, form="full"):

@@ -84,8 +84,8 @@ def test_refused_residency_selects_layout_without_handoffs(native, oracle, sizes
     finally:
         os.environ.pop("PICP_RESIDENT_BLOCKS_PER_CU")
     assert b.info()["mode"] == mode_safe
-    res = b.residency()
-    assert res["resident_blocks"] == 0 and res["handoff_grid"] > 0
+    res = b.residency()  # the layout in use has no hand-off: residency reports none
+    assert res["resident_blocks"] == 0 and res["handoff_grid"] == 0
     b.solve(threshold=THR, max_rounds=50, conv_eps=-1.0)
     from picp_amd import synth
     P = b.poses()

@@ -21,15 +21,19 @@ __global__ void bench(PicpArgs A, const float* tot0, int iters, unsigned long lo
   float R[9], t[3] = {0, 0, 0}, dx[6] = {1e-4f, 2e-4f, 3e-4f, 1e-5f, 2e-5f, 3e-5f};
   for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0f : 0.0f;
   float acc = 0.0f, chi_prev = 1e30f;
+  // the loop-carried LDS word's base value, loaded once: a global load inside the timed loop
+  // would put an L2 round trip on every iteration (the round-2 figures included one)
+  const float b0 = tot0[PICP_P_B];
+  __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
     if (MODE == 0) {  // the whole finish as the kernels run it (pose + chi_prev in registers)
       RoundOut o;
       finish_round_pose(A, s_tot, it + 1, R, t, chi_prev, o);
-      if (lane == 0) s_tot[PICP_P_B] = tot0[PICP_P_B] + R[1] * 1e-30f;  // loop-carried
+      if (lane == 0) s_tot[PICP_P_B] = b0 + R[1] * 1e-30f;  // loop-carried
     } else if (MODE == 1) {
       ldl6_solve(s_tot, dx);
-      if (lane == 0) s_tot[PICP_P_B] = tot0[PICP_P_B] + dx[5] * 1e-30f;
+      if (lane == 0) s_tot[PICP_P_B] = b0 + dx[5] * 1e-30f;
     } else if (MODE == 2) {
       apply_update(dx, R, t);
       dx[3] = R[1] * 1e-3f;
