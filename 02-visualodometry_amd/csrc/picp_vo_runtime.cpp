@@ -86,16 +86,16 @@ struct picp_vo {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // The sequence is captured once into a hipGraph and replayed (PICP_VO_GRAPH=0: enqueued launch
-  // by launch).  With the concurrent schedule (PICP_VO_OVERLAP=1, PICP_VO_CHAINS=2) the direct
-  // enqueue measured faster: the graph's replay keeps neither the streams' priorities nor the
-  // chains' phase offset.
+  // The default is the concurrent schedule (overlap on, two chains), enqueued launch by launch:
+  // a hipGraph replay keeps neither the streams' priorities nor the chains' phase offset
+  // (DESIGN.md §4.9).  The serial order (PICP_VO_OVERLAP=0 PICP_VO_CHAINS=1) is captured once
+  // into a hipGraph and replayed (PICP_VO_GRAPH=0: enqueued).  Every schedule gives the same bits.
   bool use_graph = true;
   bool graph_env = false;
   // the frame->next match in chunks by step index (chunk k = frame f0+k of every segment with
   // more than k steps), chunks 1.. on a side stream that runs beside the step chain
   std::vector<size_t> chunk_off;  // pprobs[chunk_off[k] .. chunk_off[k+1]) is chunk k
-  bool overlap = false;           // PICP_VO_OVERLAP=1 (default off: every chunk on the main stream, up front)
+  bool overlap = true;            // PICP_VO_OVERLAP=0: every chunk on the main stream, up front
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr;
   std::vector<hipEvent_t> ev_chunk;
@@ -103,7 +103,7 @@ struct picp_vo {
   // (group 0 on the handle's stream): one group's latency-bound PICP block kernel runs beside
   // another group's throughput-bound world match.  Group c starts after group c-1's first world
   // match (PICP_VO_PHASE=0: together), so the groups run out of phase.
-  int chains = 1;  // PICP_VO_CHAINS (default 1: the serial order)
+  int chains = 2;  // PICP_VO_CHAINS (1: one step chain, the serial order)
   int chains_eff = 1;  // chains for the current segments (1 when two groups would query one frame)
   bool phase = true;
   std::vector<hipStream_t> cstream;  // [chains], [0] unused (the handle's stream)
@@ -216,9 +216,8 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   }
   if (const char* e = getenv("PICP_VO_MATCH_FULL")) h->accept_only = atoi(e) != 0 ? 0 : 1;
   if (const char* e = getenv("PICP_VO_OVERLAP")) h->overlap = atoi(e) != 0;
-  // at most two groups: three or more gave poses that were not bit-identical to one group on
-  // MI355X (ROCm 7.2), with every group's ordering intact on paper; two were identical in every
-  // repetition (tools/vo_chains_check.py)
+  // at most two groups: three and four measured slower (C5 592k / 404k vs 597-600k frames/s with
+  // two, round 2)
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;

@@ -30,8 +30,12 @@ Printed JSON also carries:
                  the period from HIP events around the timed launches on the library's stream.
                  roofline.latency: the same kernel against its per-round latency floor (C2 is a
                  hand-off-latency-bound kernel).
+                 Its floor is the price list's broadcast + fan-in row scaled to the launch's blocks.
   cpu_baseline : the oracle's faithful float32 single-thread restatement (kind "port"), timed on
-                 this host on a bounded sample of the same workload.
+                 this host on a bounded sample of the same workload; cpu_baseline_all_cores the
+                 same over the box's CPU share (OMP_NUM_THREADS threads).  Every CPU figure is the
+                 median of 5 samples, and every GPU value the median of --samples (5) timed
+                 regions of K steps each, the per-sample values in "timing".
 """
 import argparse
 import json
@@ -48,6 +52,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_CORR = 20    # x,y,z,u,v float32 per correspondence-round
 HANDOFF_US = 0.8       # MI355X_MICROARCH.md price list, handoff-1to1 (idle, 8-B granule)
+FANIN_PAIR_US = 4.2    # price list, fanin: a 1->255 broadcast plus its 255->1 fan-in (idle, low end)
+FANIN_ARRIVAL_US = 0.012  # price list, fanin: ~11-13 ns per arrival
 FLOPS_PER_CORR = 160   # FP32 flops per correspondence-round (projection, J, J^T J, J^T e)
 VALU_PEAK_TFS = 157.3  # MI355X_MICROARCH.md chip table: peak FP32 vector
 
@@ -158,6 +164,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--n", type=int, default=0, help="override correspondences per frame")
     ap.add_argument("--problems", type=int, default=0, help="override frames (c4: total over ranks)")
+    ap.add_argument("--samples", type=int, default=5,
+                    help="timed regions of K steps each; value = the median (BASELINE.md: median of >= 5)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (headline)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--skip-extras", action="store_true",
@@ -265,6 +273,22 @@ def _timed(rk, torch, fn):
     return rk.max([el])[0], res
 
 
+def _timed_samples(rk, torch, fn, samples):
+    """BASELINE.md §"how measured": the timed region (barrier + sync on both sides, max over ranks)
+    repeated `samples` times; returns (median elapsed, that sample's fn() result, every elapsed)."""
+    runs = [_timed(rk, torch, fn) for _ in range(max(1, samples))]
+    order = sorted(range(len(runs)), key=lambda i: runs[i][0])
+    med = order[len(order) // 2]
+    return runs[med][0], runs[med][1], [r[0] for r in runs]
+
+
+def _sample_info(elapsed_all, steps, units_per_step, unit):
+    rates = sorted(units_per_step * steps / e for e in elapsed_all)
+    return {"samples": len(elapsed_all), "statistic": "median over %d timed regions of %d steps each" % (
+        len(elapsed_all), steps), "values": [round(r, 2) for r in rates], "unit": unit,
+        "spread": round((rates[-1] - rates[0]) / rates[len(rates) // 2], 4) if rates else None}
+
+
 def bench_frame(args, rk, torch):
     """C2 (headline) / C3: one independent frame per rank, R rounds per step."""
     import picp_amd
@@ -281,8 +305,10 @@ def bench_frame(args, rk, torch):
     for _ in range(args.warmup):
         b.solve_async(**params)
     b.sync()
-    # the K timed steps: K back-to-back fused solves on the library's stream, between HIP events
-    elapsed, (ev_ms, launch_us) = _timed(rk, torch, lambda: b.time(args.steps, **params))
+    # the K timed steps: K back-to-back fused solves on the library's stream, between HIP events;
+    # the region is timed args.samples times and the median reported (median of >= 5)
+    elapsed, (ev_ms, launch_us), el_all = _timed_samples(rk, torch, lambda: b.time(args.steps, **params),
+                                                         args.samples)
     err = rk.max([synth.se3_log_norm(b.poses()[0], T_gt[0])])[0]
 
     info = b.info()
@@ -292,7 +318,7 @@ def bench_frame(args, rk, torch):
     roof = _roofline(b, R, launch_us, pmc_name)
     roof["timed_region_event_ms"] = round(ev_ms, 4)
     if info["mode"] == "persistent":
-        roof["latency"] = _latency(launch_us, R)
+        roof["latency"] = _latency(launch_us, R, info["n_blocks"])
     value = rk.world * R * args.steps / elapsed
     out = {
         "metric": "PICP iterations/sec @ %d correspondences" % n,
@@ -317,12 +343,16 @@ def bench_frame(args, rk, torch):
             "parallelism": ("independent frames (seed 42 + rank), one process per GPU, RCCL world %d" % rk.world)
                            if rk.world > 1 else "single GPU",
         },
+        "timing": _sample_info(el_all, args.steps, rk.world * R, "iterations/s"),
         "roofline": roof,
         "pose_err_vs_gt_se3": err,
         "residency": b.residency(),
     }
     if rk.world > 1:
-        out["ranks"] = {"world_size_observed": rk.comm.world, "partition": "rank r solves frame seed 42 + r"}
+        out["ranks"] = {"world_size_observed": rk.comm.world, "partition": "rank r solves frame seed 42 + r",
+                        "scaling_note": "the N > 1 headline is weak scaling: independent replicas, one "
+                                        "frame per rank; the c4 sub-result is the strong-scaling curve "
+                                        "(the fixed 1024-frame batch split over the ranks)"}
     if not args.skip_extras:
         # diagnostic after the timed region: one solve with an event pair around its launch
         out["roofline"]["kernel_us_event_pair"] = round(b.time_single(**params), 3)
@@ -343,8 +373,7 @@ def bench_frame(args, rk, torch):
         out["keep_outliers_true"] = _keep_outliers_leg(b, T_init, T_gt, params, args.steps)
     if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(xyz, uv, T_init[0], R, args.cpu_seconds)
-        if args.workload == "c2":
-            out["cpu_baseline_all_cores"] = cpu_baseline_mt(xyz, uv, T_init[0], R, max(2.0, args.cpu_seconds / 2))
+        out["cpu_baseline_all_cores"] = cpu_baseline_mt(xyz, uv, T_init[0], R, max(2.0, args.cpu_seconds / 2))
     del b
     if args.workload == "c2" and not args.skip_extras:
         if args.stream_n > 0 and rk.world == 1:
@@ -359,6 +388,7 @@ def bench_frame(args, rk, torch):
         if rk.world == 1:
             sub.workload = "c3"
             sub.skip_extras = True
+            sub.cpu_seconds = 5.0
             c3 = bench_frame(sub, rk, torch)
             c3["roofline"] = _resident_bound(c3["roofline"])
             out["c3"] = _compact(c3)
@@ -367,7 +397,8 @@ def bench_frame(args, rk, torch):
 
 
 def _compact(d):
-    keep = ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "roofline", "cpu_baseline",
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "timing", "roofline",
+            "cpu_baseline", "cpu_baseline_all_cores",
             "pose_err_vs_gt_se3", "pose_err_vs_gt_se3_max", "kernel_us", "kernel", "traffic", "traffic_source",
             "picp_iterations_per_s", "ranks", "config")
     out = {k: d[k] for k in keep if k in d}
@@ -376,16 +407,22 @@ def _compact(d):
     return out
 
 
-def _latency(launch_us, R):
-    """C2's persistent kernel against its per-round latency floor: a round needs one reduction of
-    every block's partial to the leader and one broadcast of the new pose back (two dependent
-    cross-CU hand-offs, MI355X_MICROARCH.md handoff-1to1: 0.8 us each on an idle chip), plus the
-    compute on the critical path; the floor counts only the two hops."""
+def _latency(launch_us, R, n_blocks):
+    """The persistent kernel against its per-round communication floor.  A round is one fan-in of
+    every block's partial to the leader and one broadcast of the new pose back to every block.
+    MI355X_MICROARCH.md's price list has that exact pair as a row ("fanin": a 1->255 broadcast plus
+    its 255->1 fan-in, 4.2-4.6 us idle, the fan-in at ~11-13 ns per arrival); scaled to this
+    launch's n_blocks at 12 ns per arrival below 255, from the row's low end.  The compute on the
+    round's critical path (the linearize, the combine, the 6x6 solve) is not in the floor, so
+    frac < 1 by that much even with perfect hand-offs; two idle handoff-1to1 hops (1.6 us) are
+    the unreachable lower bound that ignores the arrival cost and is kept beside it."""
     per_round = launch_us / max(R, 1)
-    floor = 2 * HANDOFF_US
+    floor = round(max(2 * HANDOFF_US, FANIN_PAIR_US - FANIN_ARRIVAL_US * max(0, 255 - n_blocks)), 3)
     return {"per_round_us": round(per_round, 3), "floor_us": floor, "frac": round(floor / per_round, 4),
-            "floor_basis": "2 x handoff-1to1 (fan-in of the block partials + fan-out of the pose), "
-                           "MI355X_MICROARCH.md price list; compute on the critical path excluded",
+            "floor_basis": "MI355X_MICROARCH.md fanin row: 1->255 broadcast + 255->1 fan-in 4.2 us idle, "
+                           "minus %.3f us per arrival for the %d blocks of this launch; compute on the "
+                           "critical path excluded" % (FANIN_ARRIVAL_US, n_blocks),
+            "two_hop_bound_us": 2 * HANDOFF_US,
             "phases": "DESIGN.md §4.3 (stamp logs under profiles/)"}
 
 
@@ -432,7 +469,7 @@ def bench_c4(args, rk, torch):
             return r, rk.comm.allgather_batch(b, total)[0]
         return r, b.poses()
 
-    elapsed, ((ev_ms, launch_us), allT) = _timed(rk, torch, job)
+    elapsed, ((ev_ms, launch_us), allT), el_all = _timed_samples(rk, torch, job, args.samples)
     err = max(synth.se3_log_norm(b.poses()[i], bt["T_gt"][i]) for i in range(f1 - f0))
     err = rk.max([err])[0]
     mine = np.array_equal(allT[f0:f1], b.poses())  # the gather put this rank's rows in place
@@ -449,6 +486,7 @@ def bench_c4(args, rk, torch):
         "steps": args.steps,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
         "scaling": "strong",
+        "timing": _sample_info(el_all, args.steps, total * R, "iterations/s"),
         "roofline": roof,
         "pose_err_vs_gt_se3": err,
         "config": {"workload": wl["desc"], "frames_total": total, "frames_this_rank": f1 - f0,
@@ -462,6 +500,7 @@ def bench_c4(args, rk, torch):
     if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
         sz = int(bt["sizes"][0])
         out["cpu_baseline"] = cpu_baseline(bt["xyz"][:sz], bt["uv"][:sz], bt["T_init"][0], R, args.cpu_seconds)
+        out["cpu_baseline_all_cores"] = cpu_baseline_batch_mt(bt, R, args.cpu_seconds)
     return out
 
 
@@ -520,7 +559,7 @@ def bench_vo(args, rk, torch):
     vo.set_segments(my_first, my_steps, boot, threshold=THRESHOLD)
     for _ in range(max(args.warmup, 1)):
         vo.run()
-    elapsed, ev_ms = _timed(rk, torch, lambda: vo.time(args.steps))
+    elapsed, ev_ms, el_all = _timed_samples(rk, torch, lambda: vo.time(args.steps), args.samples)
     # correctness of what was timed: drift vs gt, PICP work done
     P, Rr = vo.poses(), vo.step_records()
     err, rounds, corr = 0.0, 0, 0
@@ -553,6 +592,7 @@ def bench_vo(args, rk, torch):
                    "parallelism": "contiguous segment ranges (picp_shard_range), one process per GPU"
                    if rk.world > 1 else "single GPU",
                    "block_npt": info["npt"]},
+        "timing": _sample_info(el_all, args.steps, frames_total, "frames/s"),
         "picp_iterations_per_s": round(rounds * args.steps / elapsed, 1),
         "picp_corr_rounds_per_s": round(corr * args.steps / elapsed, 1),
         "timed_region_event_ms": round(ev_ms * args.steps, 4),
@@ -564,8 +604,7 @@ def bench_vo(args, rk, torch):
                         "partition": [list(picp_amd.shard_range(len(first), rk.world, r)) for r in range(rk.world)]}
     if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
-        if args.workload == "c5":
-            out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
+        out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
     return out
 
 
@@ -603,61 +642,91 @@ def plan_only(args, rk):
                           "c4_gather_matches_single_process": gather_ok}), flush=True)
 
 
+CPU_SAMPLES = 5  # every CPU figure is the median of >= 5 samples
+
+
+def _median_rate(call, budget_s, samples=CPU_SAMPLES, warm=False):
+    """call() -> units done; run it for budget_s / samples seconds (at least once) per sample;
+    returns (median units/s, sorted per-sample rates, calls, seconds).  warm: one untimed call
+    first (thread-pool start-up)."""
+    if warm:
+        call()
+    rates, calls, t_all = [], 0, time.perf_counter()
+    for _ in range(samples):
+        units, t0 = 0, time.perf_counter()
+        while True:
+            units += call()
+            calls += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s / samples:
+                break
+        rates.append(units / el)
+    rates.sort()
+    return rates[len(rates) // 2], rates, calls, time.perf_counter() - t_all
+
+
+def _cpu_result(rate, rates, unit, cores, sample):
+    return {"value": round(rate, 3), "unit": unit, "cores": cores, "kind": "port",
+            "statistic": "median of %d samples" % len(rates), "samples": [round(r, 3) for r in rates],
+            "sample": sample}
+
+
+def _host_threads():
+    """The threads a CPU baseline may use: OMP_NUM_THREADS (16 on the GPU box = its CPU share;
+    os.cpu_count() shows the whole machine there)."""
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 64))
+
+
 def cpu_baseline_vo(seq, L, budget_s):
-    """Oracle VO loop (faithful float32, 1 thread) over whole segments of the same sequence
-    until the budget is used: frames/s."""
+    """Oracle VO loop (faithful float32, 1 thread) over whole segments of the same sequence:
+    frames/s, median of CPU_SAMPLES samples."""
     import numpy as np
     import oracle as O
     D = seq.frames(0, min(seq.n_frames, 4 * L + 1))
-    frames, t0, f0 = 0, time.perf_counter(), 0
-    while True:
+    state = {"f0": 0}
+
+    def one():
+        f0 = state["f0"]
         st = min(L, len(D["frame_off"]) - 2 - f0)
         if st < 1:
-            f0 = 0
-            continue
+            f0, st = 0, min(L, len(D["frame_off"]) - 2)
         T1 = (np.linalg.inv(D["T_cw"][f0].astype(np.float64)) @ D["T_cw"][f0 + 1]).astype(np.float32)
         O.vo_segment(seq.K, 480, 640, D["frame_off"], D["uv"], D["desc"], f0, st, np.eye(4, dtype=np.float32),
                      T1, mode=O.MODE_FAITHFUL)
-        frames += st
-        f0 += L
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "%d frames in %d-step segments of the same sequence (oracle VO loop, faithful "
-                      "float32, gcc -O3, 1 thread) in %.1f s" % (frames, L, el)}
+        state["f0"] = f0 + L
+        return st
+
+    rate, rates, calls, el = _median_rate(one, budget_s)
+    return _cpu_result(rate, rates, "frames/s", 1,
+                       "%d segments of <= %d steps of the same sequence (oracle VO loop, faithful float32, "
+                       "gcc -O3, 1 thread) in %.1f s" % (calls, L, el))
 
 
 def cpu_baseline_vo_mt(seq, L, budget_s):
     """SURVEY.md §8d all-cores variant of the C5 baseline: the oracle VO loop over independent
-    segments in parallel, one segment per host thread (OMP_NUM_THREADS threads, 16 = the GPU box's
-    CPU share).  ctypes releases the GIL around or_vo_segment, whose VO path keeps no static
-    state, so the threads run concurrently.  Timing only, never a parity oracle."""
+    segments in parallel, one segment per host thread.  ctypes releases the GIL around
+    or_vo_segment, whose VO path keeps no static state, so the threads run concurrently.  Timing
+    only, never a parity oracle."""
     import concurrent.futures as cf
     import numpy as np
     import oracle as O
-    nt = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 64))
+    nt = _host_threads()
     D = seq.frames(0, min(seq.n_frames, nt * L + 1))
     nseg = max(1, (len(D["frame_off"]) - 2) // L)
-    t0 = time.perf_counter()
 
     def worker(i):
         f0 = (i % nseg) * L
         st = min(L, len(D["frame_off"]) - 2 - f0)
         T1 = (np.linalg.inv(D["T_cw"][f0].astype(np.float64)) @ D["T_cw"][f0 + 1]).astype(np.float32)
-        done = 0
-        while time.perf_counter() - t0 < budget_s:
-            O.vo_segment(seq.K, 480, 640, D["frame_off"], D["uv"], D["desc"], f0, st,
-                         np.eye(4, dtype=np.float32), T1, mode=O.MODE_FAITHFUL)
-            done += st
-        return done
+        O.vo_segment(seq.K, 480, 640, D["frame_off"], D["uv"], D["desc"], f0, st,
+                     np.eye(4, dtype=np.float32), T1, mode=O.MODE_FAITHFUL)
+        return st
 
     with cf.ThreadPoolExecutor(max_workers=nt) as ex:
-        frames = sum(ex.map(worker, range(nt)))
-    el = time.perf_counter() - t0
-    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": nt, "kind": "port",
-            "sample": "%d frames: %d threads, each re-running one %d-step segment of the same sequence "
-                      "(oracle VO loop, faithful float32, gcc -O3) for %.1f s on %s" % (frames, nt, L, el, _cpu_model())}
+        rate, rates, calls, el = _median_rate(lambda: sum(ex.map(worker, range(nt))), budget_s, warm=True)
+    return _cpu_result(rate, rates, "frames/s", nt,
+                       "%d rounds of %d threads, each running one <= %d-step segment of the same sequence "
+                       "(oracle VO loop, faithful float32, gcc -O3) in %.1f s on %s" % (calls, nt, L, el, _cpu_model()))
 
 
 def _cpu_model():
@@ -672,50 +741,78 @@ def _cpu_model():
     return model
 
 
+KREF = [[180, 0, 320], [0, 180, 240], [0, 0, 1]]  # the synthetic generator's camera
+
+
+def _soa(xyz, uv):
+    import numpy as np
+    return [np.ascontiguousarray(xyz[:, i]) for i in range(3)] + [np.ascontiguousarray(uv[:, i]) for i in range(2)]
+
+
 def cpu_baseline_mt(xyz, uv, T_init, R, budget_s):
     """SURVEY.md §8d's all-cores CPU baseline for C2/C3: the oracle's loop with the linearize as a
-    chunked reduction over OMP_NUM_THREADS threads (the box's CPU share; os.cpu_count() shows the
-    whole machine).  Timing only; its pose is checked against the sequential oracle's."""
+    chunked reduction over the host threads.  Timing only (its summation order is not the
+    reference's)."""
     import numpy as np
     import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    x, y, z = (np.ascontiguousarray(xyz[:, i]) for i in range(3))
-    u, v = np.ascontiguousarray(uv[:, 0]), np.ascontiguousarray(uv[:, 1])
-    Kref = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
-    solves, t0 = 0, time.perf_counter()
-    while True:
-        O.solve_soa_mt(T_init, Kref, 480, 640, x, y, z, u, v, THRESHOLD, threads,
-                       mode=O.MODE_FAITHFUL, max_rounds=R, conv_eps=-1.0)
-        solves += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(solves * R / el, 3), "unit": "iterations/s", "cores": threads, "kind": "port",
-            "sample": "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, "
-                      "linearize as a chunked reduction over %d OpenMP threads, gcc -O3 "
-                      "-march=x86-64-v3) in %.1f s on %s" % (solves, R, len(x), threads, el, _cpu_model())}
+    threads = _host_threads()
+    cols = _soa(xyz, uv)
+    Kref = np.array(KREF, np.float32)
+
+    def one():
+        O.solve_soa_mt(T_init, Kref, 480, 640, *cols, THRESHOLD, threads, mode=O.MODE_FAITHFUL,
+                       max_rounds=R, conv_eps=-1.0)
+        return R
+
+    rate, rates, calls, el = _median_rate(one, budget_s, warm=True)
+    return _cpu_result(rate, rates, "iterations/s", threads,
+                       "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, linearize "
+                       "as a chunked reduction over %d OpenMP threads, gcc -O3 -march=x86-64-v3) in %.1f s on %s"
+                       % (calls, R, len(cols[0]), threads, el, _cpu_model()))
+
+
+def cpu_baseline_batch_mt(bt, R, budget_s):
+    """BASELINE.md's all-cores C4 baseline: "all-core OpenMP over problems" -- independent frames of
+    the batch solved concurrently, one per host thread (the sequential oracle solve per frame;
+    ctypes releases the GIL and or_solve_soa keeps no static state)."""
+    import concurrent.futures as cf
+    import numpy as np
+    import oracle as O
+    nt = _host_threads()
+    Kref = np.array(KREF, np.float32)
+    offs = np.concatenate([[0], np.cumsum(bt["sizes"])]).astype(np.int64)
+    nf = len(bt["sizes"])
+    frames = [_soa(bt["xyz"][offs[i]:offs[i + 1]], bt["uv"][offs[i]:offs[i + 1]]) for i in range(min(nf, nt))]
+
+    def worker(i):
+        O.solve_soa(bt["T_init"][i], Kref, 480, 640, *frames[i], THRESHOLD, mode=O.MODE_FAITHFUL,
+                    max_rounds=R, conv_eps=-1.0)
+        return R
+
+    with cf.ThreadPoolExecutor(max_workers=nt) as ex:
+        rate, rates, calls, el = _median_rate(lambda: sum(ex.map(worker, range(len(frames)))), budget_s, warm=True)
+    return _cpu_result(rate, rates, "iterations/s", nt,
+                       "%d rounds of %d frames of the batch (%d correspondences each) solved concurrently, one "
+                       "%d-round sequential oracle solve per thread (faithful float32, gcc -O3 -march=x86-64-v3) "
+                       "in %.1f s on %s" % (calls, len(frames), int(bt["sizes"][0]), R, el, _cpu_model()))
 
 
 def cpu_baseline(xyz, uv, T_init, R, budget_s):
-    """Oracle (faithful float32, sequential) single thread on one frame of the workload:
-    whole R-round solves until the time budget is used (at least one)."""
+    """Oracle (faithful float32, sequential) single thread on one frame of the workload: whole
+    R-round solves, median of CPU_SAMPLES samples (at least one solve each)."""
     import numpy as np
     import oracle as O
-    x, y, z = (np.ascontiguousarray(xyz[:, i]) for i in range(3))
-    u, v = np.ascontiguousarray(uv[:, 0]), np.ascontiguousarray(uv[:, 1])
-    Kref = np.array([[180, 0, 320], [0, 180, 240], [0, 0, 1]], np.float32)
-    solves, t0 = 0, time.perf_counter()
-    while True:
-        O.solve_soa(T_init, Kref, 480, 640, x, y, z, u, v, THRESHOLD, mode=O.MODE_FAITHFUL,
-                    max_rounds=R, conv_eps=-1.0)
-        solves += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(solves * R / el, 3), "unit": "iterations/s", "cores": 1, "kind": "port",
-            "sample": "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, "
-                      "gcc -O3 -march=x86-64-v3, 1 thread) in %.1f s on %s" % (solves, R, len(x), el,
-                                                                              _cpu_model())}
+    cols = _soa(xyz, uv)
+    Kref = np.array(KREF, np.float32)
+
+    def one():
+        O.solve_soa(T_init, Kref, 480, 640, *cols, THRESHOLD, mode=O.MODE_FAITHFUL, max_rounds=R, conv_eps=-1.0)
+        return R
+
+    rate, rates, calls, el = _median_rate(one, budget_s)
+    return _cpu_result(rate, rates, "iterations/s", 1,
+                       "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, gcc -O3 "
+                       "-march=x86-64-v3, 1 thread) in %.1f s on %s" % (calls, R, len(cols[0]), el, _cpu_model()))
 
 
 if __name__ == "__main__":

@@ -47,6 +47,23 @@ def test_library_has_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle target id
 
 
+def test_shipped_environment_switches_are_the_documented_ones():
+    """Every PICP_* variable the shipped library can read is a row of INTEGRATION.md §4, and none
+    of the diagnostic (result-changing) ones is among them (diagnostics live in
+    diagnostic builds only)."""
+    import picp_amd
+    blob = open(picp_amd.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"\x00(PICP_[A-Z0-9_]+)\x00", blob))
+    names = {n.decode() for n in names}
+    assert "PICP_MODE" in names
+    for diag in ("PICP_VO_DIAG_SKIP", "PICP_MATCH_ACCEPT_ONLY", "PICP_MATCH_EXACT"):
+        assert diag not in names, diag
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = doc[doc.index("## 4."):doc.index("## 5.")]
+    missing = sorted(n for n in names if "`%s" % n not in sec)
+    assert not missing, missing
+
+
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"), reason="no llvm-objdump")
 def test_shipped_device_code_has_no_packed_fp32_and_no_calls():
     """every kernel of the shipped library is built without packed-FP32 VALU code

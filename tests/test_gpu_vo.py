@@ -234,9 +234,10 @@ def _assert_same_bits(a, b, what):
 def test_vo_step_schedules_bit_identical(native, monkeypatch):
     """The concurrent step schedules -- the frame->next match beside the step chain
     (PICP_VO_OVERLAP=1), two step chains (PICP_VO_CHAINS=2), both -- give the serial order's
-    poses, step records and maps bit for bit, run after run.  Before the kernels were built
-    without packed FP32 (picp_internal.h PICP_KERNEL_FP32), the matcher's MFMA waves beside the
-    PICP block kernel changed its lanes 48-63 and this differed in every run."""
+    poses, step records and maps bit for bit, run after run; so does the library's default (the
+    concurrent schedule, no variable set).  Before the device code was built without packed FP32
+    (hipcc_nopk.sh), the matcher's MFMA waves beside the PICP block kernel changed its lanes 48-63
+    and this differed in every run."""
     from picp_amd.vo_synth import VOSequence, segments
     s = VOSequence(2001, obs_per_frame=2000, seed=42)
     F = s.frames(0, 2001)
@@ -244,11 +245,15 @@ def test_vo_step_schedules_bit_identical(native, monkeypatch):
     rel = [np.linalg.inv(F["T_cw"][f].astype(np.float64)) for f in first]
     boot = np.stack([[np.eye(4), rel[k] @ F["T_cw"][f + 1]] for k, f in enumerate(first)]).astype(np.float32)
     schedules = [{"PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"}, {"PICP_VO_OVERLAP": "1", "PICP_VO_CHAINS": "1"},
-                 {"PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "2"}, {"PICP_VO_OVERLAP": "1", "PICP_VO_CHAINS": "2"}]
+                 {"PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "2"}, {"PICP_VO_OVERLAP": "1", "PICP_VO_CHAINS": "2"},
+                 {"PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None}]
     ref = None
     for env in schedules:
         for k, v in env.items():
-            monkeypatch.setenv(k, v)
+            if v is None:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, v)
         outs = _vo_outputs(native, F, s.K, first, steps, boot)
         if ref is None:
             ref = outs[0]
