@@ -274,29 +274,44 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       d[6] = T.r02; d[7] = T.r12; d[8] = T.r22; d[9] = T.t0; d[10] = T.t1; d[11] = T.t2;
     }
 #endif
-    Acc2 a;
-    acc2_zero(a);
-    Cnt nr = {0u, 0u}, nd = {0u, 0u};  // counts: register items (uniform), divergent loops (lane 0)
-    accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
-    for (int i = tid; i < n_lds; i += 2 * BS) {  // LDS-staged items, in pairs
-      const int i2 = min(i + BS, n_lds - 1);
-      // scalar locals first: building the f2 operands from the LDS reads directly made the
-      // compiler round-trip them through scratch every round
-      const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
-      const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
-      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
-                      (f2){v0, v1}, true, i + BS < n_lds, a, nd);
-    }
-    for (int i = r0 + n_lds + tid; i < n; i += 2 * BS) {  // streamed remainder
-      const int i2 = min(i + BS, n - 1);
-      const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
-      const float x1 = X[base + i2], y1 = Y[base + i2], z1 = Z[base + i2], u1 = U[base + i2], v1 = V[base + i2];
-      accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
-                      (f2){v0, v1}, true, i + BS < n, a, nd);
-    }
+    // accumulation form by register-resident items per lane (picp_device.h acc_pairs): two slots
+    // for NPT 8, one slot below
     float v[PICP_NPART];
-    BSTAMP(1);
-    acc2_fold(a, v);
+    Cnt nr = {0u, 0u}, nd = {0u, 0u};  // counts: register items (uniform), divergent loops (lane 0)
+    if constexpr (acc_pairs(NPT)) {
+      Acc2 a;
+      acc2_zero(a);
+      accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
+      for (int i = tid; i < n_lds; i += 2 * BS) {  // LDS-staged items, in pairs
+        const int i2 = min(i + BS, n_lds - 1);
+        // scalar locals first: building the f2 operands from the LDS reads directly made the
+        // compiler round-trip them through scratch every round
+        const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
+        const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
+        accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
+                        (f2){v0, v1}, true, i + BS < n_lds, a, nd);
+      }
+      for (int i = r0 + n_lds + tid; i < n; i += 2 * BS) {  // streamed remainder
+        const int i2 = min(i + BS, n - 1);
+        const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
+        const float x1 = X[base + i2], y1 = Y[base + i2], z1 = Z[base + i2], u1 = U[base + i2], v1 = V[base + i2];
+        accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
+                        (f2){v0, v1}, true, i + BS < n, a, nd);
+      }
+      BSTAMP(1);
+      acc2_fold(a, v);
+    } else {
+      Acc a;
+      acc_zero(a);
+      accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
+      for (int i = tid; i < n_lds; i += BS)  // LDS-staged items
+        accumulate_item<PH>(T, C, thr, inv_thr, keep, lx[i], ly[i], lz[i], lu[i], lv[i], true, a, nd);
+      for (int i = r0 + n_lds + tid; i < n; i += BS)  // streamed remainder
+        accumulate_item<PH>(T, C, thr, inv_thr, keep, X[base + i], Y[base + i], Z[base + i], U[base + i],
+                            V[base + i], true, a, nd);
+      BSTAMP(1);
+      acc_fold(a, v);
+    }
 #if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 16)
     if (s_ldiag && round <= picp_bdiag_rounds) {
       float* d = s_ldiag + ((size_t)(round - 1) * BS + tid) * PICP_NPART;

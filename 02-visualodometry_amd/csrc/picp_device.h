@@ -203,6 +203,13 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
   }
 }
 
+// The reciprocal of the depth (ph2 == pc2 exactly): RCP_CHECK decides per pair by a wave vote;
+// RCP_FAST: the caller's vote found every depth of the section inside rcp_safe's range (rcp_rn,
+// exhaustively verified); RCP_DIV: the IEEE division.
+#define RCP_CHECK 0
+#define RCP_FAST 1
+#define RCP_DIV 2
+
 // Pinhole camera K = [fx 0 cx; 0 fy cy; 0 0 1] (the reference's K, src/cam.cpp:11-16; the
 // runtime selects this path only when K has exactly that structure).  Every term the general
 // form multiplies by one of K's zeros is an exact +-0 and K(2,2) = 1 makes ph2 == pc2, so with
@@ -219,7 +226,16 @@ __device__ __forceinline__ void accumulate_one(const Pose& T, const Cam& C, floa
 // instructions per correspondence than the general path.  KEEP (keep_outliers, compile time):
 // without it every used item has weight 1 and every other item has J = e = 0 (zeroed inputs),
 // so H and b take J itself -- bit-identical to multiplying by w in {0, 1}, 10 multiplies fewer.
-template <bool KEEP>
+// The camera-frame depth of one item in accumulate_pinhole's exact operation order (so the
+// compiler shares it with the item's projection).
+__device__ __forceinline__ float item_depth(const Pose& T, float x, float y, float z) {
+#pragma clang fp contract(off)
+  return ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;  // src/camera.h:26, row 2
+}
+
+// RCP: RCP_DIV (the IEEE division) or RCP_FAST (rcp_rn: the caller's wave vote found the depth
+// inside rcp_safe's range; the same bits).
+template <bool KEEP, int RCP = RCP_DIV>
 __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, float thr,
                                                    float inv_thr, float x, float y,
                                                    float z, float u, float v, bool in_range,
@@ -233,7 +249,7 @@ __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, 
     pc2 = ((T.r20 * x + T.r21 * y) + T.r22 * z) + T.t2;
     ph0 = C.k00 * pc0 + C.k02 * pc2;  // src/camera.h:29 without the zero terms
     ph1 = C.k11 * pc1 + C.k12 * pc2;
-    iz = 1.0f / pc2;                  // ph2 == pc2 exactly
+    iz = (RCP == RCP_FAST) ? rcp_rn(pc2) : 1.0f / pc2;  // ph2 == pc2 exactly
     const float ix = ph0 * iz;
     const float iy = ph1 * iz;
     // bitwise, not short-circuit: the same predicate without per-item exec-mask branches
@@ -427,13 +443,6 @@ __device__ __forceinline__ bool pair_rcp_safe(const Pose& T, f2 x, f2 y, f2 z) {
   return rcp_safe(d.x) & rcp_safe(d.y);
 }
 
-// The reciprocal of the depth (ph2 == pc2 exactly): RCP_CHECK decides per pair by a wave vote;
-// RCP_FAST: the caller's vote found every depth of the section inside rcp_safe's range (rcp_rn,
-// exhaustively verified); RCP_DIV: the IEEE division.
-#define RCP_CHECK 0
-#define RCP_FAST 1
-#define RCP_DIV 2
-
 template <bool KEEP, int RCP = RCP_CHECK>
 __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C, float thr,
                                                     float inv_thr, f2 x, f2 y, f2 z,
@@ -564,6 +573,89 @@ __device__ __forceinline__ void accumulate_regs(const Pose& T, const Cam& C, flo
     run(std::integral_constant<int, RCP_FAST>());
   else
     run(std::integral_constant<int, RCP_DIV>());
+}
+
+// Which accumulation form a kernel with NPT register-resident items per lane uses.  Measured on
+// MI355X with the unpacked build (profiles/r03/acc/): one slot is faster at small NPT (C5, NPT 4:
+// +2.7 %), the two-slot pair form at NPT 8 (C3 +5-9 %, C4 +17 %: its two independent
+// accumulation chains and its paired LDS/stream loops).  -DPICP_ACC_PAIRS / -DPICP_ACC_ONE force
+// one form for A/B builds.
+__host__ __device__ constexpr bool acc_pairs(int npt) {
+#if defined(PICP_ACC_PAIRS)
+  return true;
+#elif defined(PICP_ACC_ONE)
+  return false;
+#else
+  return npt >= 8;
+#endif
+}
+
+// accumulate_regs with ONE accumulator slot, item by item (the default since the device code is
+// built without packed FP32, hipcc_nopk.sh): the pair form's two slots only paid for themselves
+// as packed instructions; unpacked, they double the accumulator registers (58 instead of 29 per
+// lane) and every per-pair select.  The fast-reciprocal vote is taken once for the whole set.
+// The sum runs over the items in order k = 0 .. NPT-1 (the pair form summed even and odd items in
+// separate slots): the bits differ from it in the last place, within the H/b tolerance.
+template <int PH, int NPT>
+__device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, float thr, float inv_thr,
+                                                 bool keep, const float* xs, const float* ys,
+                                                 const float* zs, const float* us, const float* vs,
+                                                 int first, int stride, int n, Acc& a, Cnt& cnt) {
+  if constexpr (PH == PICP_V_GENERAL) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      accumulate_one(T, C, thr, keep, xs[k], ys[k], zs[k], us[k], vs[k], first + k * stride < n, a, cnt);
+  } else {
+    bool fast = true;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) fast &= rcp_safe(item_depth(T, xs[k], ys[k], zs[k]));
+    auto run = [&](auto rcp) {
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, decltype(rcp)::value>(T, C, thr, inv_thr, xs[k], ys[k], zs[k],
+                                                                           us[k], vs[k], first + k * stride < n, a, cnt);
+    };
+    if (__all(fast))
+      run(std::integral_constant<int, RCP_FAST>());
+    else
+      run(std::integral_constant<int, RCP_DIV>());
+  }
+}
+
+// One streamed (LDS or HBM) item, pinhole or general, the fast reciprocal by a vote of the lanes
+// that run this item (the loops that call it are divergent).
+template <int PH>
+__device__ __forceinline__ void accumulate_item(const Pose& T, const Cam& C, float thr, float inv_thr,
+                                                bool keep, float x, float y, float z, float u, float v,
+                                                bool in_range, Acc& a, Cnt& n) {
+  if constexpr (PH == PICP_V_GENERAL) {
+    accumulate_one(T, C, thr, keep, x, y, z, u, v, in_range, a, n);
+  } else {
+    if (__all(rcp_safe(item_depth(T, x, y, z))))
+      accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_FAST>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
+    else
+      accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_DIV>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
+  }
+}
+
+__device__ __forceinline__ void acc_zero(Acc& a) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) a.h[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
+  a.chi_in = a.chi_out = 0.0f;
+}
+
+__device__ __forceinline__ void acc_fold(const Acc& a, float v[PICP_NPART]) {
+#pragma unroll
+  for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[PICP_P_B + i] = a.b[i];
+  v[PICP_P_CHI_IN] = a.chi_in;
+  v[PICP_P_CHI_OUT] = a.chi_out;
+  v[PICP_P_N_IN] = 0.0f;
+  v[PICP_P_N_PROJ] = 0.0f;
+  v[31] = 0.0f;
 }
 
 // one correspondence with the variant chosen at compile time
@@ -753,6 +845,129 @@ __device__ __forceinline__ bool ldl6_solve(const float* tw, float dx[6]) {
 
 __device__ __forceinline__ void ldl6_solve(const float* tw, float dx[6]) {
   if (ldl6_solve<false>(tw, dx)) ldl6_solve<true>(tw, dx);  // a (near-)zero pivot: rare
+}
+
+// The damped 6x6 solve with a short dependency chain (the one-lane form is latency-bound: a
+// single wave's dependent VALU ops issue ~8 cycles apart, v_rcp_f32 ~20).  Same elimination as
+// ldl6_solve, regrouped so the reciprocal is the only thing each step waits for:
+//   forward: a[i][c] -= (a[i][j] a[c][j]) / d_j, rhs[i] -= (a[i][j] rhs[j]) / d_j -- the products
+//            are formed while v_rcp_f32(d_j) is in flight, then ONE fma per entry;
+//   back:    y_i = rhs_i / d_i and u[k][i] = a[k][i] / d_i formed off the chain, then
+//            x_k = y_k, y_i -= u[k][i] x_k -- one fma per step.
+// The chain is 2 ops per pivot + 1 per back step (18) instead of 3 + 2 (30).  Rounding differs
+// from ldl6_solve in the last bits (a product of two entries before the scale, not after); the
+// per-round pose stays within the oracle tolerance (tests/test_gpu_parity.py).
+template <bool GUARD>
+__device__ __forceinline__ bool ldl6_solve_short(const float* tw, float dx[6]) {
+  float a[6][6], rhs[6], id[6];
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int c = 0; c <= i; ++c) a[i][c] = tw[tri_index(c, i)];
+    rhs[i] = tw[PICP_P_B + i];
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const float d = a[j][j];
+    float inv = __builtin_amdgcn_rcpf(d);
+    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
+    else bad |= !(fabsf(d) > FLT_MIN);
+    id[j] = inv;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+#pragma unroll
+      for (int c = j + 1; c <= i; ++c) a[i][c] = fmaf(-(a[i][j] * a[c][j]), inv, a[i][c]);
+      rhs[i] = fmaf(-(a[i][j] * rhs[j]), inv, rhs[i]);
+    }
+  }
+  float y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) y[i] = rhs[i] * id[i];
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    const float x = y[k];
+    dx[k] = x;
+#pragma unroll
+    for (int i = 0; i < k; ++i) y[i] = fmaf(-(a[k][i] * id[i]), x, y[i]);
+  }
+  return bad;
+}
+
+__device__ __forceinline__ void ldl6_solve_short(const float* tw, float dx[6]) {
+  if (ldl6_solve_short<false>(tw, dx)) ldl6_solve_short<true>(tw, dx);
+}
+
+// DPP row_newbcast:N (gfx950): lane N of each 16-lane row, to every lane of that row.  bound_ctrl
+// set: a lane whose source is invalid would get 0, never a stale register (no source is invalid
+// here: every lane of a finishing wave is active), and no tied "old" copy is needed.
+template <int N>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xF, 0xF, true));
+}
+
+// ldl6_solve with the elimination spread over the lanes of each 16-lane row: lane r (< 6) holds
+// row r of the lower triangle (its entries right of the diagonal are never read), and step j's
+// pivot, its rhs and column j (a[c][j], c > j) reach every lane by row_newbcast.  The same
+// operations on the same operands in the same order as ldl6_solve -- a[i][c] -= f_i a[c][j],
+// f_i = a[i][j] / d_j, rhs_i -= f_i rhs_j, the back substitution from the column values each step
+// broadcast -- so the result is bit-identical; 27 DPP moves replace 15 of the 35 trailing-update
+// FMAs' serial issue and the 21 loads of the one-lane form.  Every lane of the wave must be
+// active; every lane returns the same dx (each row solves the system).
+template <bool GUARD>
+__device__ __forceinline__ bool ldl6_solve_wave(const float* tw, float dx[6]) {
+  const int r0 = (int)(__lane_id() & 15);
+  const int r = r0 < 6 ? r0 : 5;  // lanes 6-15 shadow row 5 (never broadcast from)
+  float col[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) col[c] = tw[tri_index(c, r)];
+  float rhs = tw[PICP_P_B + r];
+  float id[6], rj[6], lc[6][6];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float d, bj;
+    switch (j) {  // DPP controls are immediates
+      case 0: d = row_bcast<0>(col[0]); bj = row_bcast<0>(rhs); break;
+      case 1: d = row_bcast<1>(col[1]); bj = row_bcast<1>(rhs); break;
+      case 2: d = row_bcast<2>(col[2]); bj = row_bcast<2>(rhs); break;
+      case 3: d = row_bcast<3>(col[3]); bj = row_bcast<3>(rhs); break;
+      case 4: d = row_bcast<4>(col[4]); bj = row_bcast<4>(rhs); break;
+      default: d = row_bcast<5>(col[5]); bj = row_bcast<5>(rhs); break;
+    }
+    float inv = __builtin_amdgcn_rcpf(d);
+    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
+    else bad |= !(fabsf(d) > FLT_MIN);
+    id[j] = inv;
+    rj[j] = bj;
+    const float f = col[j] * inv;
+#pragma unroll
+    for (int c = j + 1; c < 6; ++c) {
+      float b;
+      switch (c) {
+        case 1: b = row_bcast<1>(col[j]); break;
+        case 2: b = row_bcast<2>(col[j]); break;
+        case 3: b = row_bcast<3>(col[j]); break;
+        case 4: b = row_bcast<4>(col[j]); break;
+        default: b = row_bcast<5>(col[j]); break;
+      }
+      lc[c][j] = b;  // a[c][j] after steps < j: the back substitution's U[j][c]
+      col[c] = fmaf(-f, b, col[c]);
+    }
+    rhs = fmaf(-f, bj, rhs);
+  }
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    const float x = rj[k] * id[k];
+    dx[k] = x;
+#pragma unroll
+    for (int i = 0; i < k; ++i) rj[i] = fmaf(-lc[k][i], x, rj[i]);
+  }
+  return bad;
+}
+
+__device__ __forceinline__ void ldl6_solve_wave(const float* tw, float dx[6]) {
+  if (ldl6_solve_wave<false>(tw, dx)) ldl6_solve_wave<true>(tw, dx);
 }
 
 // sin/cos of GN increment angles.  Increments are small, so the float Taylor series (exact to

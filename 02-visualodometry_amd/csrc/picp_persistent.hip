@@ -173,11 +173,18 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       v[PICP_P_N_IN] = 0.0f;
       v[PICP_P_N_PROJ] = 0.0f;
       v[31] = 0.0f;
-    } else {  // pairs of register-resident items, packed (accumulate2)
-      Acc2 a;
-      acc2_zero(a);
-      accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, PICP_PBLOCK, count, a, nc);
-      acc2_fold(a, v);
+    } else {  // NPT register-resident items per lane
+      if constexpr (acc_pairs(NPT)) {
+        Acc2 a;
+        acc2_zero(a);
+        accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, PICP_PBLOCK, count, a, nc);
+        acc2_fold(a, v);
+      } else {
+        Acc a;
+        acc_zero(a);
+        accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, PICP_PBLOCK, count, a, nc);
+        acc_fold(a, v);
+      }
     }
     const float wsum = wave_counts(wave_reduce32(v, lane), lane, nc);
     if ((lane & 1) == 0) s_wave[wave][lane >> 1] = wsum;

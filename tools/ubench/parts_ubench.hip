@@ -5,7 +5,9 @@
 using namespace picp;
 
 // MODE 0: finish_round_pose (tw in LDS, loop state in registers), 1: ldl6_solve (tw in LDS),
-//      2: apply_update (registers), 3: LDS state copy (s_st -> ns -> s_st), 4: empty loop
+//      2: apply_update (registers), 3: LDS state copy (s_st -> ns -> s_st), 4: empty loop,
+//      5: ldl6_solve_wave (tw in LDS, the elimination over a row's lanes),
+//      6: ldl6_solve_short (tw in LDS, the short-chain regrouping)
 template <int MODE>
 __global__ void bench(PicpArgs A, const float* tot0, int iters, unsigned long long* cyc, float* out) {
   __shared__ float s_tot[PICP_NPART];
@@ -34,6 +36,12 @@ __global__ void bench(PicpArgs A, const float* tot0, int iters, unsigned long lo
     } else if (MODE == 1) {
       ldl6_solve(s_tot, dx);
       if (lane == 0) s_tot[PICP_P_B] = b0 + dx[5] * 1e-30f;
+    } else if (MODE == 5) {
+      ldl6_solve_wave(s_tot, dx);
+      if (lane == 0) s_tot[PICP_P_B] = b0 + dx[5] * 1e-30f;
+    } else if (MODE == 6) {
+      ldl6_solve_short(s_tot, dx);
+      if (lane == 0) s_tot[PICP_P_B] = b0 + dx[5] * 1e-30f;
     } else if (MODE == 2) {
       apply_update(dx, R, t);
       dx[3] = R[1] * 1e-3f;
@@ -55,6 +63,43 @@ __global__ void bench(PicpArgs A, const float* tot0, int iters, unsigned long lo
   if (lane == 0) { cyc[MODE] = (t1 - t0) / iters; out[MODE] = acc; }
 }
 
+// ldl6_solve vs ldl6_solve_wave on the same systems: every lane's dx must equal the one-lane
+// solve's bits.  System v: the main() system with entry (v % 21) scaled by 1 + v * 1e-3 and b
+// perturbed; v >= 60: a zero pivot (row/col 3 zeroed) for the guarded path.
+__global__ void check(const float* tot0, int nsys, unsigned* bad, float* maxrel) {
+  __shared__ float s_tot[PICP_NPART];
+  const int lane = threadIdx.x;
+  for (int v = 0; v < nsys; ++v) {
+    if (lane < PICP_NPART) {
+      float x = tot0[lane];
+      if (lane == (v % 21)) x *= 1.0f + 1e-3f * (float)v;
+      if (lane >= PICP_P_B && lane < PICP_P_B + 6) x += 1e-4f * (float)((v * 7 + lane) % 13);
+      if (v >= 60 && lane < 21) {  // zero row/column 3: a zero pivot
+        const int rr[21] = {0,0,0,0,0,0,1,1,1,1,1,2,2,2,2,3,3,3,4,4,5};
+        const int cc[21] = {0,1,2,3,4,5,1,2,3,4,5,2,3,4,5,3,4,5,4,5,5};
+        if (rr[lane] == 3 || cc[lane] == 3) x = 0.0f;
+      }
+      s_tot[lane] = x;
+    }
+    __syncthreads();
+    float a[6], b[6], c[6];
+    ldl6_solve(s_tot, a);
+    ldl6_solve_wave(s_tot, b);
+    ldl6_solve_short(s_tot, c);
+    bool m = false;
+    float amax = 0.0f, dmax = 0.0f;
+    for (int i = 0; i < 6; ++i) {
+      m |= __float_as_uint(a[i]) != __float_as_uint(b[i]);
+      amax = fmaxf(amax, fabsf(a[i]));
+      dmax = fmaxf(dmax, fabsf(a[i] - c[i]));
+    }
+    if (lane == 0 && amax > 0.0f) atomicMax((unsigned*)maxrel, __float_as_uint(dmax / amax));
+    const unsigned long long bm = __ballot(m);
+    if (lane == 0 && bm) atomicAdd(bad, 1u);
+    __syncthreads();
+  }
+}
+
 int main() {
   PicpArgs A{};
   A.damping = 1.0f; A.min_inliers = 0; A.max_rounds = 1 << 30; A.conv_eps = -1.0f;
@@ -73,11 +118,22 @@ int main() {
     hipLaunchKernelGGL(bench<2>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
     hipLaunchKernelGGL(bench<3>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
     hipLaunchKernelGGL(bench<4>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipLaunchKernelGGL(bench<5>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
+    hipLaunchKernelGGL(bench<6>, dim3(1), dim3(64), 0, 0, A, d_tot, iters, d_cyc, d_out);
     hipDeviceSynchronize();
   }
   unsigned long long cyc[8];
   hipMemcpy(cyc, d_cyc, 64, hipMemcpyDeviceToHost);
-  printf("cycles/iter: finish_round_pose %llu  ldl6_solve %llu  apply_update %llu  state_copy %llu  empty %llu\n",
-         cyc[0], cyc[1], cyc[2], cyc[3], cyc[4]);
+  printf("cycles/iter: finish_round_pose %llu  ldl6_solve %llu  apply_update %llu  state_copy %llu  empty %llu  "
+         "ldl6_solve_wave %llu  ldl6_solve_short %llu\n", cyc[0], cyc[1], cyc[2], cyc[3], cyc[4], cyc[5], cyc[6]);
+  unsigned* d_bad; unsigned nbad = 0;
+  float* d_rel; float rel = 0.0f;
+  hipMalloc(&d_bad, 4); hipMemset(d_bad, 0, 4);
+  hipMalloc(&d_rel, 4); hipMemset(d_rel, 0, 4);
+  hipLaunchKernelGGL(check, dim3(1), dim3(64), 0, 0, d_tot, 64, d_bad, d_rel);
+  hipMemcpy(&nbad, d_bad, 4, hipMemcpyDeviceToHost);
+  hipMemcpy(&rel, d_rel, 4, hipMemcpyDeviceToHost);
+  printf("ldl6_solve_wave vs ldl6_solve: %u of 64 systems differ (4 with a zero pivot)\n", nbad);
+  printf("ldl6_solve_short vs ldl6_solve: max |ddx| / max |dx| = %.3g over the 64 systems\n", rel);
   return 0;
 }
