@@ -847,129 +847,6 @@ __device__ __forceinline__ void ldl6_solve(const float* tw, float dx[6]) {
   if (ldl6_solve<false>(tw, dx)) ldl6_solve<true>(tw, dx);  // a (near-)zero pivot: rare
 }
 
-// The damped 6x6 solve with a short dependency chain (the one-lane form is latency-bound: a
-// single wave's dependent VALU ops issue ~8 cycles apart, v_rcp_f32 ~20).  Same elimination as
-// ldl6_solve, regrouped so the reciprocal is the only thing each step waits for:
-//   forward: a[i][c] -= (a[i][j] a[c][j]) / d_j, rhs[i] -= (a[i][j] rhs[j]) / d_j -- the products
-//            are formed while v_rcp_f32(d_j) is in flight, then ONE fma per entry;
-//   back:    y_i = rhs_i / d_i and u[k][i] = a[k][i] / d_i formed off the chain, then
-//            x_k = y_k, y_i -= u[k][i] x_k -- one fma per step.
-// The chain is 2 ops per pivot + 1 per back step (18) instead of 3 + 2 (30).  Rounding differs
-// from ldl6_solve in the last bits (a product of two entries before the scale, not after); the
-// per-round pose stays within the oracle tolerance (tests/test_gpu_parity.py).
-template <bool GUARD>
-__device__ __forceinline__ bool ldl6_solve_short(const float* tw, float dx[6]) {
-  float a[6][6], rhs[6], id[6];
-  bool bad = false;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-#pragma unroll
-    for (int c = 0; c <= i; ++c) a[i][c] = tw[tri_index(c, i)];
-    rhs[i] = tw[PICP_P_B + i];
-  }
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const float d = a[j][j];
-    float inv = __builtin_amdgcn_rcpf(d);
-    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
-    else bad |= !(fabsf(d) > FLT_MIN);
-    id[j] = inv;
-#pragma unroll
-    for (int i = j + 1; i < 6; ++i) {
-#pragma unroll
-      for (int c = j + 1; c <= i; ++c) a[i][c] = fmaf(-(a[i][j] * a[c][j]), inv, a[i][c]);
-      rhs[i] = fmaf(-(a[i][j] * rhs[j]), inv, rhs[i]);
-    }
-  }
-  float y[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) y[i] = rhs[i] * id[i];
-#pragma unroll
-  for (int k = 5; k >= 0; --k) {
-    const float x = y[k];
-    dx[k] = x;
-#pragma unroll
-    for (int i = 0; i < k; ++i) y[i] = fmaf(-(a[k][i] * id[i]), x, y[i]);
-  }
-  return bad;
-}
-
-__device__ __forceinline__ void ldl6_solve_short(const float* tw, float dx[6]) {
-  if (ldl6_solve_short<false>(tw, dx)) ldl6_solve_short<true>(tw, dx);
-}
-
-// DPP row_newbcast:N (gfx950): lane N of each 16-lane row, to every lane of that row.  bound_ctrl
-// set: a lane whose source is invalid would get 0, never a stale register (no source is invalid
-// here: every lane of a finishing wave is active), and no tied "old" copy is needed.
-template <int N>
-__device__ __forceinline__ float row_bcast(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xF, 0xF, true));
-}
-
-// ldl6_solve with the elimination spread over the lanes of each 16-lane row: lane r (< 6) holds
-// row r of the lower triangle (its entries right of the diagonal are never read), and step j's
-// pivot, its rhs and column j (a[c][j], c > j) reach every lane by row_newbcast.  The same
-// operations on the same operands in the same order as ldl6_solve -- a[i][c] -= f_i a[c][j],
-// f_i = a[i][j] / d_j, rhs_i -= f_i rhs_j, the back substitution from the column values each step
-// broadcast -- so the result is bit-identical; 27 DPP moves replace 15 of the 35 trailing-update
-// FMAs' serial issue and the 21 loads of the one-lane form.  Every lane of the wave must be
-// active; every lane returns the same dx (each row solves the system).
-template <bool GUARD>
-__device__ __forceinline__ bool ldl6_solve_wave(const float* tw, float dx[6]) {
-  const int r0 = (int)(__lane_id() & 15);
-  const int r = r0 < 6 ? r0 : 5;  // lanes 6-15 shadow row 5 (never broadcast from)
-  float col[6];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) col[c] = tw[tri_index(c, r)];
-  float rhs = tw[PICP_P_B + r];
-  float id[6], rj[6], lc[6][6];
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    float d, bj;
-    switch (j) {  // DPP controls are immediates
-      case 0: d = row_bcast<0>(col[0]); bj = row_bcast<0>(rhs); break;
-      case 1: d = row_bcast<1>(col[1]); bj = row_bcast<1>(rhs); break;
-      case 2: d = row_bcast<2>(col[2]); bj = row_bcast<2>(rhs); break;
-      case 3: d = row_bcast<3>(col[3]); bj = row_bcast<3>(rhs); break;
-      case 4: d = row_bcast<4>(col[4]); bj = row_bcast<4>(rhs); break;
-      default: d = row_bcast<5>(col[5]); bj = row_bcast<5>(rhs); break;
-    }
-    float inv = __builtin_amdgcn_rcpf(d);
-    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
-    else bad |= !(fabsf(d) > FLT_MIN);
-    id[j] = inv;
-    rj[j] = bj;
-    const float f = col[j] * inv;
-#pragma unroll
-    for (int c = j + 1; c < 6; ++c) {
-      float b;
-      switch (c) {
-        case 1: b = row_bcast<1>(col[j]); break;
-        case 2: b = row_bcast<2>(col[j]); break;
-        case 3: b = row_bcast<3>(col[j]); break;
-        case 4: b = row_bcast<4>(col[j]); break;
-        default: b = row_bcast<5>(col[j]); break;
-      }
-      lc[c][j] = b;  // a[c][j] after steps < j: the back substitution's U[j][c]
-      col[c] = fmaf(-f, b, col[c]);
-    }
-    rhs = fmaf(-f, bj, rhs);
-  }
-#pragma unroll
-  for (int k = 5; k >= 0; --k) {
-    const float x = rj[k] * id[k];
-    dx[k] = x;
-#pragma unroll
-    for (int i = 0; i < k; ++i) rj[i] = fmaf(-lc[k][i], x, rj[i]);
-  }
-  return bad;
-}
-
-__device__ __forceinline__ void ldl6_solve_wave(const float* tw, float dx[6]) {
-  if (ldl6_solve_wave<false>(tw, dx)) ldl6_solve_wave<true>(tw, dx);
-}
-
 // sin/cos of GN increment angles.  Increments are small, so the float Taylor series (exact to
 // float rounding for |a| <= 1/16: next term a^9/9! < 1e-16) avoids sincosf's range reduction
 // on the critical path; ONE test for the three angles keeps the common case straight-line (three
@@ -980,9 +857,8 @@ __device__ __forceinline__ void taylor_sincos(float a, float* s, float* c) {
   *c = fmaf(a2, fmaf(a2, fmaf(a2, fmaf(a2, 1.0f / 40320.0f, -1.0f / 720.0f), 1.0f / 24.0f), -0.5f), 1.0f);
 }
 
-// src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
-// src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
-__device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
+// src/defs.h:100-136 v2tEuler's rotation: Rd = Rx(a)*Ry(b)*Rz(c) (float) of dx[3..5].
+__device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3]) {
   float sa, ca, sb, cb, sc, cc;
   if (fabsf(dx[3]) <= 0.0625f && fabsf(dx[4]) <= 0.0625f && fabsf(dx[5]) <= 0.0625f) {
     taylor_sincos(dx[3], &sa, &ca);
@@ -996,7 +872,6 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
   // Rd = Rx(a)*Ry(b)*Rz(c) in closed form: the same products and sums as the 3x3 products
   // of src/defs.h:133 with their structural zeros and ones folded away (x*1 = x, x+0 = x).
   const float sasb = sa * sb, casb = ca * sb;
-  float Rd[3][3];
   Rd[0][0] = cb * cc;
   Rd[0][1] = -(cb * sc);
   Rd[0][2] = sb;
@@ -1006,6 +881,13 @@ __device__ __forceinline__ void apply_update(const float dx[6], float R[9], floa
   Rd[2][0] = sa * sc - casb * cc;
   Rd[2][1] = casb * sc + sa * cc;
   Rd[2][2] = ca * cb;
+}
+
+// src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
+// src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
+__device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
+  float Rd[3][3];
+  update_rotation(dx, Rd);
   float Rn[9], tn[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
