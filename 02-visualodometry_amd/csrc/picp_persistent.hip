@@ -26,7 +26,15 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 #define PICP_MAX_PBLK 256   // max blocks per problem in this mode (sweep registers)
-#define PICP_PBLOCK 512     // threads per block: 8 waves, 2 per SIMD (<= 256 VGPRs)
+#define PICP_PBLOCK 512     // the partition's unit: npt items per lane of a 512-thread block
+// -DPICP_PWIDE=1 (A/B): npt 8 (4096 items per block, C3) as 1024 threads x 4 items, four waves
+// per SIMD instead of two within 128 VGPRs.  Alone, that linearize is 11 % faster than 512 x 8
+// (tools/ubench/lin_ubench.hip at 97 VGPRs); inside this kernel, squeezed to 128 VGPRs next to the
+// hand-off code, the leader's linearize + publish took 3.9 instead of 3.5 us and C3 did not move
+// (139-141k it/s both; profiles/r03/pwide/).
+#ifndef PICP_PWIDE
+#define PICP_PWIDE 0
+#endif
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
 // never hoisted out of a spin loop)
@@ -65,16 +73,16 @@ __device__ __forceinline__ bool timed_out(unsigned long long deadline) {
   return __builtin_amdgcn_s_memrealtime() > deadline;
 }
 
-template <int NPT, int PH>
-__global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
+template <int NPT, int PH, int BS>
+__global__ __launch_bounds__(BS) void picp_persistent_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
     unsigned long long* gpart, unsigned long long* gpose, unsigned int* err, unsigned int* tagbase,
     unsigned long long timeout_ticks) {
-  __shared__ double s_red[PICP_NPART][PICP_PBLOCK / 64];  // term-major: one row per combining lane
+  __shared__ double s_red[PICP_NPART][BS / 64];  // term-major: one row per combining lane
   __shared__ float s_tot[PICP_NPART];
-  __shared__ float s_wave[PICP_PBLOCK / 64][PICP_NPART];
+  __shared__ float s_wave[BS / 64][PICP_NPART];
   __shared__ float s_pose[12];
   __shared__ int s_done;
   __shared__ int s_tmo;  // a wait of this block timed out (the error word is for the host)
@@ -104,7 +112,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const int i = tid + k * PICP_PBLOCK;
+    const int i = tid + k * BS;
     const int ic = min(i, max(count - 1, 0));
     xs[k] = X[base + ic];
     ys[k] = Y[base + ic];
@@ -177,12 +185,12 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       if constexpr (acc_pairs(NPT)) {
         Acc2 a;
         acc2_zero(a);
-        accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, PICP_PBLOCK, count, a, nc);
+        accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc);
         acc2_fold(a, v);
       } else {
         Acc a;
         acc_zero(a);
-        accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, PICP_PBLOCK, count, a, nc);
+        accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc);
         acc_fold(a, v);
       }
     }
@@ -192,7 +200,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
     if (tid < PICP_NPART) {
       float sum = s_wave[0][tid];
 #pragma unroll
-      for (int w = 1; w < PICP_PBLOCK / 64; ++w) sum += s_wave[w][tid];
+      for (int w = 1; w < BS / 64; ++w) sum += s_wave[w][tid];
       __hip_atomic_store(my_part0 + (epoch & 1) * part_stride + tid, granule(tbase + epoch, sum), RLX_AGENT);
     }
     PSTAMP(1);
@@ -201,7 +209,7 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
       // ---- 2. sweep the problem's partials: 16-B sc1 loads of granule pairs (2c, 2c+1) of
       //         blocks g + NG*i (c = tid&15, g = tid>>4); each 8-B half carries its own tag ----
       const int c = tid & 15, g = tid >> 4;
-      constexpr int NG = PICP_PBLOCK / 16;  // block groups swept in parallel
+      constexpr int NG = BS / 16;  // block groups swept in parallel
       constexpr int MAXG = PICP_MAX_PBLK / NG;
       const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(prob_part0 + (epoch & 1) * part_stride), 0, nblk * PICP_NPART * 8, 0x00020000);
@@ -273,12 +281,12 @@ __global__ __launch_bounds__(PICP_PBLOCK) void picp_persistent_kernel(
           for (int i = 0; i < 3; ++i) pt[i] = s_pose[9 + i];
         }
         if (lane < PICP_NPART) {
-          double ws[PICP_PBLOCK / 64];  // every load issued before the first add
+          double ws[BS / 64];  // every load issued before the first add
 #pragma unroll
-          for (int w = 0; w < PICP_PBLOCK / 64; ++w) ws[w] = s_red[lane][w];
+          for (int w = 0; w < BS / 64; ++w) ws[w] = s_red[lane][w];
           double t = ws[0];
 #pragma unroll
-          for (int w = 1; w < PICP_PBLOCK / 64; ++w) t += ws[w];
+          for (int w = 1; w < BS / 64; ++w) t += ws[w];
           s_tot[lane] = total_word(A, lane, t);  // lane e converts total e
         }
         __builtin_amdgcn_wave_barrier();
@@ -353,12 +361,20 @@ extern "C" hipError_t picp_debug_pstamps(unsigned long long* out, size_t n_words
 // ------------------------------- host launch wrapper -------------------------------
 extern "C" int picp_persistent_block(void) { return PICP_PBLOCK; }
 
+// npt (items per lane of a 512-thread block) -> the kernel's items per lane and block size
+template <int N>
+struct PShape {
+  static constexpr int npt = (PICP_PWIDE && N == 8) ? 4 : N;
+  static constexpr int bs = (PICP_PWIDE && N == 8) ? 1024 : PICP_PBLOCK;
+};
+
 template <int N>
 static const void* persistent_kernel_n(int var) {
+  constexpr int T = PShape<N>::npt, B = PShape<N>::bs;
   switch (var) {
-    case PICP_V_PINHOLE: return (const void*)picp_persistent_kernel<N, PICP_V_PINHOLE>;
-    case PICP_V_PINHOLE_KEEP: return (const void*)picp_persistent_kernel<N, PICP_V_PINHOLE_KEEP>;
-    default: return (const void*)picp_persistent_kernel<N, PICP_V_GENERAL>;
+    case PICP_V_PINHOLE: return (const void*)picp_persistent_kernel<T, PICP_V_PINHOLE, B>;
+    case PICP_V_PINHOLE_KEEP: return (const void*)picp_persistent_kernel<T, PICP_V_PINHOLE_KEEP, B>;
+    default: return (const void*)picp_persistent_kernel<T, PICP_V_GENERAL, B>;
   }
 }
 
@@ -378,7 +394,8 @@ extern "C" hipError_t picp_persistent_occupancy(int npt, const float K[9], int* 
       default: return hipErrorInvalidValue;
     }
     int occ = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, PICP_PBLOCK, 0);
+    const hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, npt == 8 ? PShape<8>::bs : PICP_PBLOCK, 0);
     if (e != hipSuccess) return e;
     best = (best < 0 || occ < best) ? occ : best;
   }
@@ -395,9 +412,10 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              unsigned long long timeout_ticks) {
   if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
   const int var = picp_variant(args->K, args->keep_outliers);
-#define PICP_LAUNCH_PV(N, PV)                                                                           \
-  hipLaunchKernelGGL((picp_persistent_kernel<N, PV>), dim3(grid), dim3(PICP_PBLOCK), 0, stream, X, Y, Z, \
-                     U, V, *args, st_in, st_out, gpart, gpose, err, tagbase, timeout_ticks)
+#define PICP_LAUNCH_PV(N, PV)                                                                      \
+  hipLaunchKernelGGL((picp_persistent_kernel<PShape<N>::npt, PV, PShape<N>::bs>), dim3(grid),      \
+                     dim3(PShape<N>::bs), 0, stream, X, Y, Z, U, V, *args, st_in, st_out, gpart, gpose, \
+                     err, tagbase, timeout_ticks)
 #define PICP_LAUNCH_P(N)                                                            \
   if (var == PICP_V_PINHOLE) PICP_LAUNCH_PV(N, PICP_V_PINHOLE);                     \
   else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_PV(N, PICP_V_PINHOLE_KEEP);      \
