@@ -588,13 +588,30 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
           load_b(buf, (sg + kb) * 32 + r, b1);
           bt[kb] = b1[0];
         }
+        // Software-pipelined over the group's BT x RB MFMA blocks: block q+1's MFMA is issued
+        // before block q's result is tested, into the other of two accumulators, so the MFMA's
+        // latency runs under the previous block's max tree and vote instead of stalling the wave
+        // (the blocks used to be issued and consumed one at a time: an s_nop 11 after every MFMA).
+        // -DMM_NO_PIPE: one at a time (A/B).
+        constexpr int NQB = BT * RB;
+        mm_f16v accs[2];
+#ifndef MM_NO_PIPE
+        accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[0], (mm_f16v){}, 0, 0, 0);
+#endif
 #pragma unroll
-        for (int kb = 0; kb < BT; ++kb) {
-          const int sub = sg + kb;
-          const int col = sub * 32 + r;
-#pragma unroll
-          for (int rb = 0; rb < RB; ++rb) {
-            const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[kb], (mm_f16v){}, 0, 0, 0);
+        for (int q = 0; q < NQB; ++q) {
+          const int kb = q / RB, rb = q - kb * RB;
+          const int col = (sg + kb) * 32 + r;
+#ifndef MM_NO_PIPE
+          if (q + 1 < NQB)
+            accs[(q + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[(q + 1) % RB], bt[(q + 1) / RB],
+                                                                        (mm_f16v){}, 0, 0, 0);
+          const mm_f16v acc = accs[q & 1];
+#else
+          const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[kb], (mm_f16v){}, 0, 0, 0);
+          (void)accs;
+#endif
+          {
             // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
             // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
             // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
