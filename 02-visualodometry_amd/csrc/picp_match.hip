@@ -588,21 +588,22 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
           load_b(buf, (sg + kb) * 32 + r, b1);
           bt[kb] = b1[0];
         }
-        // Software-pipelined over the group's BT x RB MFMA blocks: block q+1's MFMA is issued
-        // before block q's result is tested, into the other of two accumulators, so the MFMA's
-        // latency runs under the previous block's max tree and vote instead of stalling the wave
-        // (the blocks used to be issued and consumed one at a time: an s_nop 11 after every MFMA).
-        // -DMM_NO_PIPE: one at a time (A/B).
+        // The group's BT x RB MFMA blocks are issued and consumed one at a time (an s_nop 11 after
+        // every MFMA); other waves of the SIMD fill the wait.  -DMM_PIPE (A/B): software-pipelined,
+        // block q+1's MFMA issued into a second accumulator before block q's result is tested.
+        // Measured slower: the second accumulator costs a wave per SIMD (RB = 2: 108 -> 131
+        // VGPRs, 4 -> 3 waves) and 1,024 x 2,000 x 2,000 took 353 instead of 316 us, C5 619k
+        // instead of 632-635k frames/s (profiles/r03/mab/).
         constexpr int NQB = BT * RB;
         mm_f16v accs[2];
-#ifndef MM_NO_PIPE
+#ifdef MM_PIPE
         accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[0], (mm_f16v){}, 0, 0, 0);
 #endif
 #pragma unroll
         for (int q = 0; q < NQB; ++q) {
           const int kb = q / RB, rb = q - kb * RB;
           const int col = (sg + kb) * 32 + r;
-#ifndef MM_NO_PIPE
+#ifdef MM_PIPE
           if (q + 1 < NQB)
             accs[(q + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[(q + 1) % RB], bt[(q + 1) / RB],
                                                                         (mm_f16v){}, 0, 0, 0);
