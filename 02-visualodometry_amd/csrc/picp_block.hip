@@ -481,7 +481,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
         }
       }
 #else
-      finish_round_pose(A, s_tot, round, pr, pt, chi_prev, o);
+      finish_round_pose<PICP_FINISH_WAVE>(A, s_tot, round, pr, pt, chi_prev, o);
 #endif
       if (s_tmo) o.done = 1;  // a partner wait timed out: stop (the host reports the error)
 #if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 8)

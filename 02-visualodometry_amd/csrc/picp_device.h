@@ -847,6 +847,78 @@ __device__ __forceinline__ void ldl6_solve(const float* tw, float dx[6]) {
   if (ldl6_solve<false>(tw, dx)) ldl6_solve<true>(tw, dx);  // a (near-)zero pivot: rare
 }
 
+// DPP row_newbcast:N (gfx950): lane N of each 16-lane row, to every lane of that row.  bound_ctrl
+// set: a lane whose source is invalid would get 0, never a stale register (no source is invalid
+// here: every lane of a finishing wave is active), and no tied "old" copy is needed.
+template <int N>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xF, 0xF, true));
+}
+
+// ldl6_solve with the elimination spread over the lanes of each 16-lane row: lane r (< 6) holds
+// row r of the lower triangle (its entries right of the diagonal are never read), and step j's
+// pivot, its rhs and column j (a[c][j], c > j) reach every lane by row_newbcast.  The same
+// operations on the same operands in the same order as ldl6_solve -- a[i][c] -= f_i a[c][j],
+// f_i = a[i][j] / d_j, rhs_i -= f_i rhs_j, the back substitution from the column values each step
+// broadcast -- so the result is bit-identical; 27 DPP moves replace 15 of the 35 trailing-update
+// FMAs' serial issue and the 21 loads of the one-lane form.  Every lane of the wave must be
+// active; every lane returns the same dx (each row solves the system).
+template <bool GUARD>
+__device__ __forceinline__ bool ldl6_solve_wave(const float* tw, float dx[6]) {
+  const int r0 = (int)(__lane_id() & 15);
+  const int r = r0 < 6 ? r0 : 5;  // lanes 6-15 shadow row 5 (never broadcast from)
+  float col[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) col[c] = tw[tri_index(c, r)];
+  float rhs = tw[PICP_P_B + r];
+  float id[6], rj[6], lc[6][6];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float d, bj;
+    switch (j) {  // DPP controls are immediates
+      case 0: d = row_bcast<0>(col[0]); bj = row_bcast<0>(rhs); break;
+      case 1: d = row_bcast<1>(col[1]); bj = row_bcast<1>(rhs); break;
+      case 2: d = row_bcast<2>(col[2]); bj = row_bcast<2>(rhs); break;
+      case 3: d = row_bcast<3>(col[3]); bj = row_bcast<3>(rhs); break;
+      case 4: d = row_bcast<4>(col[4]); bj = row_bcast<4>(rhs); break;
+      default: d = row_bcast<5>(col[5]); bj = row_bcast<5>(rhs); break;
+    }
+    float inv = __builtin_amdgcn_rcpf(d);
+    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
+    else bad |= !(fabsf(d) > FLT_MIN);
+    id[j] = inv;
+    rj[j] = bj;
+    const float f = col[j] * inv;
+#pragma unroll
+    for (int c = j + 1; c < 6; ++c) {
+      float b;
+      switch (c) {
+        case 1: b = row_bcast<1>(col[j]); break;
+        case 2: b = row_bcast<2>(col[j]); break;
+        case 3: b = row_bcast<3>(col[j]); break;
+        case 4: b = row_bcast<4>(col[j]); break;
+        default: b = row_bcast<5>(col[j]); break;
+      }
+      lc[c][j] = b;  // a[c][j] after steps < j: the back substitution's U[j][c]
+      col[c] = fmaf(-f, b, col[c]);
+    }
+    rhs = fmaf(-f, bj, rhs);
+  }
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    const float x = rj[k] * id[k];
+    dx[k] = x;
+#pragma unroll
+    for (int i = 0; i < k; ++i) rj[i] = fmaf(-lc[k][i], x, rj[i]);
+  }
+  return bad;
+}
+
+__device__ __forceinline__ void ldl6_solve_wave(const float* tw, float dx[6]) {
+  if (ldl6_solve_wave<false>(tw, dx)) ldl6_solve_wave<true>(tw, dx);
+}
+
 // sin/cos of GN increment angles.  Increments are small, so the float Taylor series (exact to
 // float rounding for |a| <= 1/16: next term a^9/9! < 1e-16) avoids sincosf's range reduction
 // on the critical path; ONE test for the three angles keeps the common case straight-line (three
@@ -933,6 +1005,9 @@ struct RoundOut {
 // reads -- the pose R (column-major) / t and chi_prev -- is carried in registers by the finishing
 // wave (every lane computes the same values; no LDS state round trip on the critical path).
 // tw may be LDS.
+// WAVE: the caller is a whole wave with every lane active (the block and persistent kernels'
+// finishing wave): the elimination runs over each 16-lane row (ldl6_solve_wave, bit-identical).
+template <bool WAVE = false>
 __device__ __forceinline__ void finish_round_pose(const PicpArgs& A, const float* tw, int j, float R[9],
                                                   float t[3], float& chi_prev, RoundOut& o) {
   o.chi_in = tw[PICP_P_CHI_IN];
@@ -946,7 +1021,10 @@ __device__ __forceinline__ void finish_round_pose(const PicpArgs& A, const float
     return;
   }
   float dx[6];
-  ldl6_solve(tw, dx);      // :96 (damping folded in by total_word), :102
+  if constexpr (WAVE)
+    ldl6_solve_wave(tw, dx);  // :96 (damping folded in by total_word), :102
+  else
+    ldl6_solve(tw, dx);
   apply_update(dx, R, t);  // :103
   o.ok = 1;
   o.done = 0;

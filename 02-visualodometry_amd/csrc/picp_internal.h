@@ -83,6 +83,12 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 // ...) from inlining into the kernel, and the calls cost C2 18 % and C5 80 % (round-3 pass).
 // `make PK=1` restores packed code (-DPICP_ALLOW_PK) for A/B builds.
 
+// The finishing wave's 6x6 solve: 1 = over each 16-lane row by DPP row_newbcast
+// (picp_device.h ldl6_solve_wave, bit-identical to the one-lane form), 0 = one lane (A/B).
+#ifndef PICP_FINISH_WAVE
+#define PICP_FINISH_WAVE 1
+#endif
+
 // Diagnostic build only (-DPICP_KFENCE): explicit agent-scope acquire at the start and release at
 // the end of the VO path's kernels, to test whether kernel-boundary visibility is what differs
 // between schedules.

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           // the wave finishes the round (every lane the same values, loop state in registers)
           RoundOut o;
           PSTAMP(4);
-          finish_round_pose(A, s_tot, (int)epoch, pr, pt, chi_prev, o);
+          finish_round_pose<PICP_FINISH_WAVE>(A, s_tot, (int)epoch, pr, pt, chi_prev, o);
           PSTAMP(5);
           if (s_tmo) o.done = 1;  // a sweep timed out
           // ---- publish the new pose (and the done flag): lane l < 16 owns word l ----

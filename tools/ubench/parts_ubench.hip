@@ -57,78 +57,6 @@ __device__ __forceinline__ void ldl6_solve_short(const float* tw, float dx[6]) {
   if (ldl6_solve_short<false>(tw, dx)) ldl6_solve_short<true>(tw, dx);
 }
 
-// DPP row_newbcast:N (gfx950): lane N of each 16-lane row, to every lane of that row.  bound_ctrl
-// set: a lane whose source is invalid would get 0, never a stale register (no source is invalid
-// here: every lane of a finishing wave is active), and no tied "old" copy is needed.
-template <int N>
-__device__ __forceinline__ float row_bcast(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + N, 0xF, 0xF, true));
-}
-
-// ldl6_solve with the elimination spread over the lanes of each 16-lane row: lane r (< 6) holds
-// row r of the lower triangle (its entries right of the diagonal are never read), and step j's
-// pivot, its rhs and column j (a[c][j], c > j) reach every lane by row_newbcast.  The same
-// operations on the same operands in the same order as ldl6_solve -- a[i][c] -= f_i a[c][j],
-// f_i = a[i][j] / d_j, rhs_i -= f_i rhs_j, the back substitution from the column values each step
-// broadcast -- so the result is bit-identical; 27 DPP moves replace 15 of the 35 trailing-update
-// FMAs' serial issue and the 21 loads of the one-lane form.  Every lane of the wave must be
-// active; every lane returns the same dx (each row solves the system).
-template <bool GUARD>
-__device__ __forceinline__ bool ldl6_solve_wave(const float* tw, float dx[6]) {
-  const int r0 = (int)(__lane_id() & 15);
-  const int r = r0 < 6 ? r0 : 5;  // lanes 6-15 shadow row 5 (never broadcast from)
-  float col[6];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) col[c] = tw[tri_index(c, r)];
-  float rhs = tw[PICP_P_B + r];
-  float id[6], rj[6], lc[6][6];
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    float d, bj;
-    switch (j) {  // DPP controls are immediates
-      case 0: d = row_bcast<0>(col[0]); bj = row_bcast<0>(rhs); break;
-      case 1: d = row_bcast<1>(col[1]); bj = row_bcast<1>(rhs); break;
-      case 2: d = row_bcast<2>(col[2]); bj = row_bcast<2>(rhs); break;
-      case 3: d = row_bcast<3>(col[3]); bj = row_bcast<3>(rhs); break;
-      case 4: d = row_bcast<4>(col[4]); bj = row_bcast<4>(rhs); break;
-      default: d = row_bcast<5>(col[5]); bj = row_bcast<5>(rhs); break;
-    }
-    float inv = __builtin_amdgcn_rcpf(d);
-    if (GUARD) inv = (fabsf(d) > FLT_MIN) ? inv : 0.0f;
-    else bad |= !(fabsf(d) > FLT_MIN);
-    id[j] = inv;
-    rj[j] = bj;
-    const float f = col[j] * inv;
-#pragma unroll
-    for (int c = j + 1; c < 6; ++c) {
-      float b;
-      switch (c) {
-        case 1: b = row_bcast<1>(col[j]); break;
-        case 2: b = row_bcast<2>(col[j]); break;
-        case 3: b = row_bcast<3>(col[j]); break;
-        case 4: b = row_bcast<4>(col[j]); break;
-        default: b = row_bcast<5>(col[j]); break;
-      }
-      lc[c][j] = b;  // a[c][j] after steps < j: the back substitution's U[j][c]
-      col[c] = fmaf(-f, b, col[c]);
-    }
-    rhs = fmaf(-f, bj, rhs);
-  }
-#pragma unroll
-  for (int k = 5; k >= 0; --k) {
-    const float x = rj[k] * id[k];
-    dx[k] = x;
-#pragma unroll
-    for (int i = 0; i < k; ++i) rj[i] = fmaf(-lc[k][i], x, rj[i]);
-  }
-  return bad;
-}
-
-__device__ __forceinline__ void ldl6_solve_wave(const float* tw, float dx[6]) {
-  if (ldl6_solve_wave<false>(tw, dx)) ldl6_solve_wave<true>(tw, dx);
-}
-
 // apply_update for ONE element of the new pose: e in 0..11 of [R column-major | t] (lanes of a
 // finishing wave take e = lane & 15, e >= 12 clamped: those lanes publish nothing).  The element's
 // products and sums are apply_update's own, in its order, so the value is bit-identical to
