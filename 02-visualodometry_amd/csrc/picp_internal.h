@@ -83,10 +83,13 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 // ...) from inlining into the kernel, and the calls cost C2 18 % and C5 80 % (round-3 pass).
 // `make PK=1` restores packed code (-DPICP_ALLOW_PK) for A/B builds.
 
-// The finishing wave's 6x6 solve: 1 = over each 16-lane row by DPP row_newbcast
-// (picp_device.h ldl6_solve_wave, bit-identical to the one-lane form), 0 = one lane (A/B).
+// The finishing wave's 6x6 solve: 0 = one lane (ldl6_solve), 1 = over each 16-lane row by DPP
+// row_newbcast (picp_device.h ldl6_solve_wave).  The two give the same bits on every workload
+// (tools/pose_dump.py); the row form is faster alone (624-680 vs 708-732 cycles) but not in the
+// kernels: C2 210.5-217.0k vs 218.7-220.3k it/s, C5 625.5-627.0k vs 630.3-633.2k frames/s
+// (profiles/r03/finish/).  A/B builds: -DPICP_FINISH_WAVE=1.
 #ifndef PICP_FINISH_WAVE
-#define PICP_FINISH_WAVE 1
+#define PICP_FINISH_WAVE 0
 #endif
 
 // Diagnostic build only (-DPICP_KFENCE): explicit agent-scope acquire at the start and release at
