@@ -35,6 +35,10 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #ifndef PICP_PWIDE
 #define PICP_PWIDE 0
 #endif
+// Followers' pose wait: two polls in flight this many s_sleep units (64 clocks) apart (0: one)
+#ifndef PICP_POSE_STAGGER
+#define PICP_POSE_STAGGER 8
+#endif
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
 // never hoisted out of a spin loop)
@@ -151,6 +155,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   const bool keep = A.keep_outliers != 0;
 
   float chi_prev = FLT_MAX;  // the leader's loop state besides the pose (exec/icp_test.cpp:89)
+  unsigned long long pose_sink = 0, pa = 0, pb = 0;  // the follower's pose polls (PICP_POSE_STAGGER)
   for (unsigned epoch = 1; !s_done; ++epoch) {
     // every wait of this round is bounded from the round's start (a whole solve may take far
     // longer than timeout_ticks at large max_rounds; one round never does)
@@ -326,6 +331,34 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
       // ---- 3. wait for the leader's pose of this round (one wave, 16 lanes) ----
       if (wave == 0) {
         unsigned long long gp = 0;
+#if PICP_POSE_STAGGER > 0
+        // Two polls in flight, PICP_POSE_STAGGER x 64 clocks apart: each poll is re-issued as soon
+        // as it has been checked, so the pair keeps its offset and the pose is seen within about
+        // half a round trip of landing instead of a whole one (two polls issued together, checked
+        // in turn, measured no gain in round 2: they stay together).  Every lane loads (lanes >= 16
+        // repeat granule 15), so the waits count exactly one poll; the poll still in flight at the
+        // exit keeps its registers until the next round's wait consumes them (pose_sink), so
+        // nothing waits on it.
+        const int gl = lane < PICP_POSE_GRAN ? lane : PICP_POSE_GRAN - 1;
+        auto poll = [&]() -> unsigned long long { return __hip_atomic_load(prob_pose + gl, RLX_AGENT); };
+        auto good = [&](unsigned long long v) { return __all((unsigned)(v >> 32) == tbase + epoch); };
+        pose_sink ^= pa ^ pb;  // last round's polls: long complete
+        pa = poll();
+        __builtin_amdgcn_s_sleep(PICP_POSE_STAGGER);
+        bool tmo = false;
+        for (;;) {
+          pb = poll();
+          if (good(pa)) { gp = pa; break; }
+          pa = poll();
+          if (good(pb)) { gp = pb; break; }
+          if (timed_out(deadline)) { tmo = true; break; }
+        }
+        if (tmo) {
+          if (lane == 0) __hip_atomic_store(errw, 2u, RLX_AGENT);
+          gp = lane == 12 ? 1u : 0u;  // force done
+          if (lane < 12) gp = __float_as_uint(s_pose[lane]);
+        }
+#else
         for (;;) {
           bool ok = true;
           if (lane < PICP_POSE_GRAN) {
@@ -341,6 +374,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           }
           PICP_POLL_PAUSE();
         }
+#endif
         if (lane < 12) s_pose[lane] = __uint_as_float((unsigned)gp);
         if (lane == 12) s_done = (int)(unsigned)gp;
       }
@@ -348,6 +382,8 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
       PSTAMP(2);
     }
   }
+  // an opaque never-true test keeps the follower's last in-flight poll alive to here
+  if (timeout_ticks == ~0ull && (pose_sink ^ pa ^ pb) == 1ull) s_pose[0] = 0.0f;
 }
 
 #ifdef PICP_STAMPS
