@@ -67,8 +67,8 @@ __device__ __forceinline__ float wave_counts(float wsum, int lane, const Cnt& c)
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // Two accumulation slots per lane: correspondences are processed in PAIRS, item A in .x and
-// item B in .y of every value, so each arithmetic step of both is ONE packed fp32 instruction
-// (v_pk_mul/add/fma_f32: two exact IEEE operations, no operand shuffles); the slots are folded
+// item B in .y of every value (written as float2 math: packed-FP32 instructions until the device
+// code was built without them, picp_internal.h; now two scalar chains); the slots are folded
 // once per thread at the end.
 struct Acc2 {
   f2 h[21];
@@ -428,7 +428,7 @@ __device__ __forceinline__ void acc2_stats(f2 chi, bool inlA, bool inlB, bool va
 }
 
 // A pair of correspondences, pinhole K: accumulate_pinhole's exact arithmetic with every
-// elementwise step packed (A in .x, B in .y).  Only the correctly rounded reciprocal, the
+// elementwise step written on float2 (A in .x, B in .y).  Only the correctly rounded reciprocal, the
 // compares and the selects stay per item.  Contraction is off exactly where the oracle has it
 // off (gate and Jacobian), so both items are bit-identical to the scalar path.
 // The camera-frame depth of a pair, in the exact operation order of accumulate_pinhole2 (so the
@@ -512,7 +512,7 @@ __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C,
   acc2_normal<true, KEEP>(J0, J1, e0, e1, w, a);
 }
 
-// A pair of correspondences, general K: per-item math (item_general), packed accumulation.
+// A pair of correspondences, general K: per-item math (item_general), paired accumulation.
 __device__ __forceinline__ void accumulate_general2(const Pose& T, const Cam& C, float thr, bool keep,
                                                     f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
                                                     bool inB, Acc2& a, Cnt& n) {

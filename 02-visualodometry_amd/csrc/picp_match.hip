@@ -7,9 +7,10 @@
 // (src/my_utilities.h:44-46,100-103).  The distance is summed over the dims in order with FP
 // contraction off, so indices, distances and accept flags are bit-identical to the CPU oracle.
 //
-// Two queries per lane, their descriptors in registers as float2 pairs, so the subtract, square
-// and in-order accumulation of both run as packed fp32 (v_pk_add_f32 / v_pk_mul_f32: two exact
-// IEEE ops per lane per instruction -- FMA contraction is off, so the bits equal the oracle's);
+// Two queries per lane, their descriptors in registers as float2 pairs (the subtract, square and
+// in-order accumulation of both written on float2; scalar instructions since the device code is
+// built without packed FP32, picp_internal.h -- FMA contraction is off, so the bits equal the
+// oracle's);
 // set 2 is streamed through LDS in tiles shared by the 512 queries of a block, one broadcast LDS
 // read feeding both queries.  Batched: blockIdx.y = problem (ragged sets).
 #include <hip/hip_runtime.h>
