@@ -406,9 +406,12 @@ def _batch_mode(native, sizes, mode, **kw):
 
 @pytest.mark.parametrize("n,of,keep,conv", [(100000, 0.0, 0, -1.0), (100000, 0.3, 1, -1.0),
                                             (1000000, 0.3, 0, -1.0), (3000, 0.0, 0, 1e-4),
-                                            (257, 0.0, 0, -1.0), (1, 0.0, 0, -1.0)])
+                                            (257, 0.0, 0, -1.0), (1, 0.0, 0, -1.0),
+                                            (250000, 0.3, 0, -1.0), (500000, 0.0, 1, 1e-5)])
 def test_persistent_and_graph_modes_agree_with_oracle(native, oracle, n, of, keep, conv):
-    """Single-launch persistent solve vs one-launch-per-round graph solve vs the oracle."""
+    """Single-launch persistent solve vs one-launch-per-round graph solve vs the oracle.  The
+    sizes cover every register-resident shape: 1 item per lane (100k), 2 (250k) and 4 (500k) --
+    the one-slot accumulation -- and 8 (1M) -- the pair form (picp_device.h acc_pairs)."""
     synth = _synth()
     p = synth.make_problem(n, seed=77, outlier_frac=of, pixel_noise=0.5, shuffle=False)
     res = {}
