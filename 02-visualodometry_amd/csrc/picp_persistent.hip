@@ -39,6 +39,9 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #ifndef PICP_POSE_STAGGER
 #define PICP_POSE_STAGGER 8
 #endif
+#ifndef PICP_POSE_NPOLL  // polls in flight in the followers' pose wait (2 or 3), when staggered
+#define PICP_POSE_NPOLL 2
+#endif
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
 // never hoisted out of a spin loop)
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   const bool keep = A.keep_outliers != 0;
 
   float chi_prev = FLT_MAX;  // the leader's loop state besides the pose (exec/icp_test.cpp:89)
-  unsigned long long pose_sink = 0, pa = 0, pb = 0;  // the follower's pose polls (PICP_POSE_STAGGER)
+  unsigned long long pose_sink = 0, pa = 0, pb = 0, pc = 0;  // the follower's pose polls (PICP_POSE_STAGGER)
   for (unsigned epoch = 1; !s_done; ++epoch) {
     // every wait of this round is bounded from the round's start (a whole solve may take far
     // longer than timeout_ticks at large max_rounds; one round never does)
@@ -342,16 +345,30 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         const int gl = lane < PICP_POSE_GRAN ? lane : PICP_POSE_GRAN - 1;
         auto poll = [&]() -> unsigned long long { return __hip_atomic_load(prob_pose + gl, RLX_AGENT); };
         auto good = [&](unsigned long long v) { return __all((unsigned)(v >> 32) == tbase + epoch); };
-        pose_sink ^= pa ^ pb;  // last round's polls: long complete
+        pose_sink ^= pa ^ pb ^ pc;  // last round's polls: long complete
+        bool tmo = false;
         pa = poll();
         __builtin_amdgcn_s_sleep(PICP_POSE_STAGGER);
-        bool tmo = false;
-        for (;;) {
+        if constexpr (PICP_POSE_NPOLL >= 3) {
           pb = poll();
-          if (good(pa)) { gp = pa; break; }
-          pa = poll();
-          if (good(pb)) { gp = pb; break; }
-          if (timed_out(deadline)) { tmo = true; break; }
+          __builtin_amdgcn_s_sleep(PICP_POSE_STAGGER);
+          for (;;) {
+            pc = poll();
+            if (good(pa)) { gp = pa; break; }
+            pa = poll();
+            if (good(pb)) { gp = pb; break; }
+            pb = poll();
+            if (good(pc)) { gp = pc; break; }
+            if (timed_out(deadline)) { tmo = true; break; }
+          }
+        } else {
+          for (;;) {
+            pb = poll();
+            if (good(pa)) { gp = pa; break; }
+            pa = poll();
+            if (good(pb)) { gp = pb; break; }
+            if (timed_out(deadline)) { tmo = true; break; }
+          }
         }
         if (tmo) {
           if (lane == 0) __hip_atomic_store(errw, 2u, RLX_AGENT);
@@ -383,7 +400,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
     }
   }
   // an opaque never-true test keeps the follower's last in-flight poll alive to here
-  if (timeout_ticks == ~0ull && (pose_sink ^ pa ^ pb) == 1ull) s_pose[0] = 0.0f;
+  if (timeout_ticks == ~0ull && (pose_sink ^ pa ^ pb ^ pc) == 1ull) s_pose[0] = 0.0f;
 }
 
 #ifdef PICP_STAMPS
