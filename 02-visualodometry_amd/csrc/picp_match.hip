@@ -295,6 +295,42 @@ __device__ __forceinline__ unsigned mm_mask16_ge0(const mm_f16v& acc) {
   return m;
 }
 
+// The same candidates as mm_mask16_ge0 in 16 instructions instead of 32, laid out by ROW: bit
+// 8k + y is set iff element i = 4k + y is >= 0, and 8k + y = (i & 3) + 8 (i >> 2) is that
+// element's row offset within its 32-row half (the caller adds 32 rb + 4 hf), so a candidate's
+// row is one add from its bit index.  v_perm_b32 selector 9 / 11 turns the sign bit of src1 /
+// src0 into a 0x00 / 0xFF byte: eight perms give two element flags each, four more gather
+// W_y = [neg(4k + y), k = 0..3] as bytes, and three bfi merge bit y of byte k from W_y.  The
+// selectors and masks sit in SGPRs (no VOP3 literals on gfx9; one SGPR per instruction).  The
+// caller has already read every accumulator element (the max tree), so the MFMA result hazard is
+// resolved.  -DMM_MASK_CARRY restores the carry form (A/B builds).
+__device__ __forceinline__ unsigned mm_mask16_rows(const mm_f16v& acc) {
+  unsigned t, u, v, m;  // W_0 in m, W_y (y > 0) in t, merged as each is done: four temporaries
+  asm("v_perm_b32 %[t], %[a4], %[a0], %[s1]\n\t"  // byte 0 = neg(a0), byte 1 = neg(a4)
+      "v_perm_b32 %[u], %[a12], %[a8], %[s1]\n\t"  // byte 0 = neg(a8), byte 1 = neg(a12)
+      "v_perm_b32 %[v], %[a5], %[a1], %[s1]\n\t"
+      "v_perm_b32 %[m], %[u], %[t], %[s2]\n\t"  // W_0 = bytes neg(0), neg(4), neg(8), neg(12)
+      "v_perm_b32 %[u], %[a13], %[a9], %[s1]\n\t"
+      "v_perm_b32 %[t], %[a6], %[a2], %[s1]\n\t"
+      "v_perm_b32 %[v], %[u], %[v], %[s2]\n\t"  // W_1
+      "v_perm_b32 %[u], %[a14], %[a10], %[s1]\n\t"
+      "v_bfi_b32 %[m], %[k1], %[m], %[v]\n\t"  // bit 0 of each byte from W_0, bits 1.. from W_1
+      "v_perm_b32 %[t], %[u], %[t], %[s2]\n\t"  // W_2
+      "v_perm_b32 %[v], %[a7], %[a3], %[s1]\n\t"
+      "v_perm_b32 %[u], %[a15], %[a11], %[s1]\n\t"
+      "v_bfi_b32 %[m], %[k3], %[m], %[t]\n\t"
+      "v_perm_b32 %[v], %[u], %[v], %[s2]\n\t"  // W_3
+      "v_bfi_b32 %[m], %[k7], %[m], %[v]\n\t"
+      "v_bfi_b32 %[m], %[m], 0, %[kf]"  // ~neg & 0x0f0f0f0f: the candidates
+      : [t] "=&v"(t), [u] "=&v"(u), [v] "=&v"(v), [m] "=&v"(m)
+      : [a0] "v"(acc[0]), [a1] "v"(acc[1]), [a2] "v"(acc[2]), [a3] "v"(acc[3]), [a4] "v"(acc[4]),
+        [a5] "v"(acc[5]), [a6] "v"(acc[6]), [a7] "v"(acc[7]), [a8] "v"(acc[8]), [a9] "v"(acc[9]),
+        [a10] "v"(acc[10]), [a11] "v"(acc[11]), [a12] "v"(acc[12]), [a13] "v"(acc[13]),
+        [a14] "v"(acc[14]), [a15] "v"(acc[15]), [s1] "s"(0x0C0C0B09u), [s2] "s"(0x05040100u),
+        [k1] "s"(0x01010101u), [k3] "s"(0x03030303u), [k7] "s"(0x07070707u), [kf] "s"(0x0F0F0F0Fu));
+  return m;
+}
+
 // RAD = 1: the accept-only (radius) form for callers that consume only accepted[] and the
 // best_idx of accepted queries (the VO sequence): pass 1 is skipped and the candidates are the
 // references within a fixed radius of the query (mm_radius below); best_idx, best_dist and
@@ -630,16 +666,25 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #else
             if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
 #endif
-              // the candidate mask in two instructions per element (the max tree above has
-              // already read every accumulator, so the asm is not the MFMA result's first reader);
-              // a wave vote per element instead (skip the elements no lane has a candidate in)
+              // the candidate mask in one instruction per element, bit = row offset (the max tree
+              // above has already read every accumulator, so the asm is not the MFMA result's
+              // first reader; the carry form took two per element); a wave vote per element instead (skip the elements no lane has a candidate in)
               // measured 1.6x slower: 16 uniform branches, and 140 VGPRs cost a wave per SIMD
+#ifdef MM_MASK_CARRY
               unsigned m = mm_mask16_ge0(acc);
               while (m) {
                 const int i = 15 - __builtin_ctz(m);
                 m &= m - 1;
                 push(32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf, (int)(t0 + col));
               }
+#else
+              unsigned m = mm_mask16_rows(acc);  // bit = the element's row offset
+              while (m) {
+                const int off = __builtin_ctz(m);
+                m &= m - 1;
+                push(32 * rb + 4 * hf + off, (int)(t0 + col));
+              }
+#endif
             }
           }
         }
