@@ -679,10 +679,15 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
               }
 #else
               unsigned m = mm_mask16_rows(acc);  // bit = the element's row offset
+              // push() with the row offset added into the packed entry, and no branch on a full
+              // list: past LCAP the entry overwrites the last slot, and c_n > LCAP then sends the
+              // wave's queries to the full scan (the scatter below), so no kept entry is lost
+              const unsigned pbase = ((unsigned)(32 * rb + 4 * hf) << 26) | (unsigned)(t0 + col);
               while (m) {
-                const int off = __builtin_ctz(m);
+                const unsigned off = (unsigned)__builtin_ctz(m);
                 m &= m - 1;
-                push(32 * rb + 4 * hf + off, (int)(t0 + col));
+                lane_list[min(c_n, LCAP - 1)] = (int)(pbase + (off << 26));
+                ++c_n;
               }
 #endif
             }
