@@ -26,6 +26,8 @@
 // split = 4 uses 256-thread blocks (BS = 256), two per CU from DIFFERENT problems: while one
 // problem's parts exchange and solve (the CU idle in split = 2), the other's compute; the
 // hardware issues the older block first, so the two settle into alternating phases.
+#include <type_traits>
+
 #include "picp_device.h"
 
 using namespace picp;
@@ -105,13 +107,149 @@ extern "C" hipError_t picp_debug_bdiag_set(float* buf, int n_problems, int round
 #define BDIAG_PTR (s_diag + (size_t)(round - 1) * BDIAG_REC)
 #endif
 
-template <int NPT, int PH, int BS>
+// The VO step's gather fused into the block kernel (VoT = VoArgs; the separate kernel is
+// vo_gather_kernel, picp_vo.hip, which this restates): the next frame's observations that the
+// world match accepted, compacted in observation order, become the block's items directly --
+// items below NPT*BS into the registers (item o -> lane o % BS, slot o / BS, through an LDS
+// slice of VOG_SLICE items per pass), the rest into the LDS stage -- instead of a kernel writing the SoA planes
+// and this one reading them back.  Items past n take the last item's values as the plane loads'
+// clamp did.  Needs n <= NPT*BS + lds_items and frames of <= VOG_CHUNKS*BS observations (the
+// host's check).  Writes a.probs[s] (the append reads n) and returns n.
+struct NoVo {};
+#define VOG_CHUNKS 8  // observation chunks of BS held in registers: 4096 at BS 512
+#define VOG_SLICE 256  // items per pass of the register transfer
+template <int NPT, int BS>
+__device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, float* xs, float* ys, float* zs,
+                                               float* us, float* vs, float* lx, float* ly, float* lz,
+                                               float* lu, float* lv, int lds_items) {
+  constexpr int NW = BS / 64;
+  __shared__ int s_wc[VOG_CHUNKS][NW];          // flagged observations per (chunk, wave)
+  __shared__ float s_sl[5][VOG_SLICE];          // the items of one pass
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const VoSegment G = a.segs[s];
+  const int64_t base = (int64_t)s * a.cap_c;
+  int64_t nn = 0, on = 0;
+  if (t < G.steps) {  // a finished segment: an empty problem (its result is never read)
+    on = a.frame_off[G.f0 + t + 1];
+    nn = a.frame_off[G.f0 + t + 2] - on;
+  }
+  // every chunk's loads first (accept flag, map index, pixel; then the map point)
+  bool fl[VOG_CHUNKS];
+  int jb[VOG_CHUNKS];
+  float px[VOG_CHUNKS], py[VOG_CHUNKS], pz[VOG_CHUNKS];
+  float2 pu[VOG_CHUNKS];
+#pragma unroll
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
+    const int64_t i = (int64_t)c * BS + tid;
+    fl[c] = i < nn && a.wm_acc[on + i] != 0;
+    jb[c] = (i < nn) ? a.wm_bi[on + i] : 0;
+    pu[c] = (i < nn) ? a.uv[on + i] : make_float2(0.0f, 0.0f);
+  }
+#pragma unroll
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
+    const int64_t j = G.map_off + (fl[c] ? jb[c] : 0);
+    px[c] = fl[c] ? a.map_xyz[3 * j + 0] : 0.0f;
+    py[c] = fl[c] ? a.map_xyz[3 * j + 1] : 0.0f;
+    pz[c] = fl[c] ? a.map_xyz[3 * j + 2] : 0.0f;
+  }
+  // the ordered compaction of all chunks with one barrier: per (chunk, wave) counts, then each
+  // flagged observation's output index = flagged before its chunk + before its wave + its lane rank
+  int rk[VOG_CHUNKS];
+#pragma unroll
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
+    const unsigned long long m = __ballot(fl[c]);
+    rk[c] = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wc[c][w] = __popcll(m);
+  }
+  __syncthreads();
+  int n = 0;
+#pragma unroll
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      pre += (k < w) ? s_wc[c][k] : 0;
+      tot += s_wc[c][k];
+    }
+    rk[c] += n + pre;
+    n += tot;
+  }
+  // items past the registers go straight to the LDS stage
+  const int r0 = NPT * BS;
+#pragma unroll
+  for (int c = 0; c < VOG_CHUNKS; ++c)
+    if (fl[c] && rk[c] >= r0 && rk[c] - r0 < lds_items) {
+      const int o = rk[c] - r0;
+      lx[o] = px[c];
+      ly[o] = py[c];
+      lz[o] = pz[c];
+      lu[o] = pu[c].x;
+      lv[o] = pu[c].y;
+    }
+  // register slot k = o / BS: the items pass by pass through an LDS slice of VOG_SLICE items
+  // (five planes of 5 KB: beside this block a CU still holds four matcher blocks); lanes whose
+  // slot is past item n - 1 take that item's values (the plane loads' clamp)
+  const int last = max(n - 1, 0);
+  const int qlast = last / VOG_SLICE;
+  float lastv[5];
+  for (int q = 0; q <= qlast && q * VOG_SLICE < NPT * BS; ++q) {  // uniform: n is the block's
+#pragma unroll
+    for (int c = 0; c < VOG_CHUNKS; ++c)
+      if (fl[c] && rk[c] / VOG_SLICE == q) {
+        const int o = rk[c] - q * VOG_SLICE;
+        s_sl[0][o] = px[c];
+        s_sl[1][o] = py[c];
+        s_sl[2][o] = pz[c];
+        s_sl[3][o] = pu[c].x;
+        s_sl[4][o] = pu[c].y;
+      }
+    __syncthreads();
+    constexpr int HPS = BS / VOG_SLICE;  // passes per register slot
+    const int k = q / HPS, o = tid - (q % HPS) * VOG_SLICE;
+#pragma unroll
+    for (int kk = 0; kk < NPT; ++kk)  // register-indexed writes unrolled into selects
+      if (kk == k && o >= 0 && o < VOG_SLICE) {
+        xs[kk] = s_sl[0][o];
+        ys[kk] = s_sl[1][o];
+        zs[kk] = s_sl[2][o];
+        us[kk] = s_sl[3][o];
+        vs[kk] = s_sl[4][o];
+      }
+    if (q == qlast) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) lastv[v] = s_sl[v][last - q * VOG_SLICE];
+    }
+    __syncthreads();
+  }
+  if (qlast * VOG_SLICE >= NPT * BS) {  // item n - 1 is in the LDS stage
+    lastv[0] = lx[last - NPT * BS];
+    lastv[1] = ly[last - NPT * BS];
+    lastv[2] = lz[last - NPT * BS];
+    lastv[3] = lu[last - NPT * BS];
+    lastv[4] = lv[last - NPT * BS];
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (k * BS + tid > last) {
+      xs[k] = lastv[0];
+      ys[k] = lastv[1];
+      zs[k] = lastv[2];
+      us[k] = lastv[3];
+      vs[k] = lastv[4];
+    }
+  if (tid == 0) a.probs[s] = PicpProblem{base, (int32_t)n, 0, 1, 0};
+  return n;
+}
+
+template <int NPT, int PH, int BS, typename VoT = NoVo>
 __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
-    unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks) {
+    unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks,
+    const VoT vo, int vo_t) {
+  constexpr bool VOG = std::is_same<VoT, VoArgs>::value;  // the VO step's gather fused in
   PICP_KFENCE_IN();
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   // wave sums, term-major: the lane combining term e reads its BS/64 wave sums as 16-B loads
@@ -130,9 +268,11 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     p = (s / split) * 8 + ((int)blockIdx.x & 7);
     if (p >= n_problems) return;  // grid padding (whole partner groups only)
   }
-  int64_t base;
-  int n;
-  if (A.uniform) {
+  int64_t base = 0;
+  int n = 0;
+  if constexpr (VOG) {
+    // set by vo_gather_items below (split is 1)
+  } else if (A.uniform) {
     base = (int64_t)p * A.stride_u;
     n = A.n_u;
   } else {
@@ -176,26 +316,31 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
 
   // the problem, loaded once into registers (coalesced: item = tid + k*BLOCK)
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
-#pragma unroll
-  for (int k = 0; k < NPT; ++k) {
-    const int ic = min(tid + k * BS, max(n - 1, 0));
-    xs[k] = X[base + ic];
-    ys[k] = Y[base + ic];
-    zs[k] = Z[base + ic];
-    us[k] = U[base + ic];
-    vs[k] = V[base + ic];
-  }
-
   // items NPT*BLOCK .. NPT*BLOCK + n_lds - 1 are staged in LDS once (read every round at LDS
   // latency); any beyond that are streamed from L2/MALL every round
   const int r0 = NPT * BS;
-  const int n_lds = max(0, min(n - r0, lds_items));
   float* lx = s_lds;
   float* ly = s_lds + lds_items;
   float* lz = s_lds + 2 * lds_items;
   float* lu = s_lds + 3 * lds_items;
   float* lv = s_lds + 4 * lds_items;
-  for (int i = tid; i < n_lds; i += BS) {
+  if constexpr (VOG) {
+    const int s = vo.seg0 + p;
+    base = (int64_t)s * vo.cap_c;
+    n = vo_gather_items<NPT, BS>(vo, s, vo_t, xs, ys, zs, us, vs, lx, ly, lz, lu, lv, lds_items);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int ic = min(tid + k * BS, max(n - 1, 0));
+      xs[k] = X[base + ic];
+      ys[k] = Y[base + ic];
+      zs[k] = Z[base + ic];
+      us[k] = U[base + ic];
+      vs[k] = V[base + ic];
+    }
+  }
+  const int n_lds = max(0, min(n - r0, lds_items));
+  for (int i = tid; i < n_lds && !VOG; i += BS) {
     lx[i] = X[base + r0 + i];
     ly[i] = Y[base + r0 + i];
     lz[i] = Z[base + r0 + i];
@@ -620,7 +765,8 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
       hipFuncSetAttribute((const void*)picp_block_kernel<N, P, B>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                           (int)lds_bytes);                                                                 \
     hipLaunchKernelGGL((picp_block_kernel<N, P, B>), dim3(grid), dim3(B), lds_bytes, stream, X, Y, Z, U, V, \
-                       *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, tagbase, timeout_ticks); \
+                       *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, tagbase, timeout_ticks, \
+                       NoVo{}, 0);                                                                     \
   }
 #define PICP_LAUNCH_BV(N, B)                                                              \
   if (var == PICP_V_PINHOLE) PICP_LAUNCH_B3(N, PICP_V_PINHOLE, B)                           \
@@ -642,5 +788,48 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
 #undef PICP_LAUNCH_B
 #undef PICP_LAUNCH_BV
 #undef PICP_LAUNCH_B3
+  return hipGetLastError();
+}
+
+// The VO step's PICP with its gather fused in (vo_gather_items): segments a->seg0 .. + n_seg of
+// step t, one 512-thread block each, npt register items per lane and the LDS stage sized for
+// max_obs (every item of a frame of <= max_obs observations is on-chip).  The caller checks
+// picp_vo_block_fusable(npt, max_obs) first; otherwise it runs vo_gather_kernel + the plain launch.
+extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs) {
+  int lds_items = 0;
+  block_lds_bytes(npt, 1, (int)max_obs, &lds_items);
+  return max_obs <= (int64_t)VOG_CHUNKS * PICP_BBLOCK && max_obs <= (int64_t)npt * PICP_BBLOCK + lds_items &&
+         (npt == 1 || npt == 2 || npt == 4 || npt == 8);
+}
+
+extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
+                                           const PicpArgs* args, int64_t max_obs) {
+  if (!a || !args || a->n_seg <= 0 || !picp_vo_block_fusable(npt, max_obs)) return hipErrorInvalidValue;
+  int lds_items = 0;
+  const size_t lds_bytes = block_lds_bytes(npt, 1, (int)max_obs, &lds_items);
+  const int var = picp_variant(args->K, args->keep_outliers);
+#define PICP_LAUNCH_VB3(N, P)                                                                               \
+  {                                                                                                        \
+    if (lds_bytes > 65536)                                                                                 \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>,                       \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);                     \
+    hipLaunchKernelGGL((picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>), dim3(a->n_seg), dim3(PICP_BBLOCK),  \
+                       lds_bytes, stream, a->X, a->Y, a->Z, a->U, a->V, *args, a->probs + a->seg0,          \
+                       a->st_in + a->seg0, (PicpState*)a->st_out + a->seg0, lds_items, 1, a->n_seg,         \
+                       nullptr, nullptr, nullptr, 0ull, *a, t);                                            \
+  }
+#define PICP_LAUNCH_VB(N)                                                        \
+  if (var == PICP_V_PINHOLE) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE)                   \
+  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE_KEEP)    \
+  else PICP_LAUNCH_VB3(N, PICP_V_GENERAL)
+  switch (npt) {
+    case 1: PICP_LAUNCH_VB(1); break;
+    case 2: PICP_LAUNCH_VB(2); break;
+    case 4: PICP_LAUNCH_VB(4); break;
+    case 8: PICP_LAUNCH_VB(8); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef PICP_LAUNCH_VB
+#undef PICP_LAUNCH_VB3
   return hipGetLastError();
 }

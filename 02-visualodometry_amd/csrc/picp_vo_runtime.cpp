@@ -38,6 +38,9 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         unsigned long long* xg, unsigned int* err,
                                         unsigned int* tagbase, unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
+extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs);
+extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
+                                           const PicpArgs* args, int64_t max_obs);
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
 
 static_assert(sizeof(picp_vo_step) == sizeof(VoStep), "picp_vo_step must mirror VoStep");
@@ -110,6 +113,10 @@ struct picp_vo {
   std::vector<hipEvent_t> ev_cj;     // [chains]: group c's end (join), [0]: fork
   std::vector<hipEvent_t> ev_ph;     // [chains]: group c's first world match done
   int accept_only = 1;  // the sequence reads only accepted matches (PICP_VO_MATCH_FULL=1: full form)
+  // the step's gather runs inside the PICP block kernel (picp_launch_vo_block) when every frame's
+  // items fit on-chip; PICP_VO_FUSE=0 keeps vo_gather_kernel + the plain block launch (A/B: the
+  // same items in the same order, the same bits)
+  bool fuse = true;
   bool guard = false;
   std::vector<VoGuarded> guards;
 #ifdef PICP_VO_DIAG
@@ -220,6 +227,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   // two, round 2)
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
+  if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
@@ -557,6 +565,11 @@ static hipError_t vo_enqueue(picp_vo* h) {
   }
   if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const int C = std::min(h->chains_eff, h->n_seg);
+#ifdef PICP_VO_DIAG
+  const bool fused = false;  // vo_snap and PICP_VO_DIAG_SKIP need the gather's planes and launch
+#else
+  const bool fused = h->fuse && picp_vo_block_fusable(h->npt, h->max_obs);
+#endif
   if (e == hipSuccess && C > 1) e = hipEventRecord(h->ev_cj[0], h->stream);  // fork
   for (int c = 0; c < C && e == hipSuccess; ++c) {
     hipStream_t st = (c == 0) ? h->stream : h->cstream[c];
@@ -573,11 +586,15 @@ static hipError_t vo_enqueue(picp_vo* h) {
                                  V.map_n1, V.map_n2, h->wprobs_d + s0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
                                  h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
-      if (e == hipSuccess && !(skip & 1)) e = picp_launch_vo_gather(st, &V, t);
-      if (e == hipSuccess && !(skip & 4))
-        e = picp_launch_block(st, V.n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs + s0,
-                              V.st_in + s0, (PicpState*)V.st_out + s0, (int)h->max_obs, 1, nullptr, nullptr,
-                              nullptr, 0);
+      if (fused) {
+        if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs);
+      } else {
+        if (e == hipSuccess && !(skip & 1)) e = picp_launch_vo_gather(st, &V, t);
+        if (e == hipSuccess && !(skip & 4))
+          e = picp_launch_block(st, V.n_seg, h->npt, V.X, V.Y, V.Z, V.U, V.V, &h->pargs, V.probs + s0,
+                                V.st_in + s0, (PicpState*)V.st_out + s0, (int)h->max_obs, 1, nullptr, nullptr,
+                                nullptr, 0);
+      }
 #ifdef PICP_VO_DIAG
       if (e == hipSuccess) e = vo_snap(h, st, t, s0, s1);
 #endif

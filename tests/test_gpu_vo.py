@@ -261,6 +261,37 @@ def test_vo_step_schedules_bit_identical(native, monkeypatch):
             _assert_same_bits(ref, o, str(env))
 
 
+@pytest.mark.parametrize("obs", [600, 2000, 2300])
+def test_vo_fused_gather_bit_identical(native, monkeypatch, obs):
+    """The step's gather inside the PICP block kernel (default; the items reach registers and the
+    LDS stage without the SoA planes) gives the separate gather kernel's poses, step records and
+    maps bit for bit, in the serial order and the default schedule.  600 observations per frame:
+    one register item per lane and most items in the LDS stage; 2300: four per lane, the rest in
+    the stage."""
+    from picp_amd.vo_synth import VOSequence, segments
+    n = 401
+    s = VOSequence(n, obs_per_frame=obs, seed=7)
+    F = s.frames(0, n)
+    first, steps = segments(n, 40)
+    rel = [np.linalg.inv(F["T_cw"][f].astype(np.float64)) for f in first]
+    boot = np.stack([[np.eye(4), rel[k] @ F["T_cw"][f + 1]] for k, f in enumerate(first)]).astype(np.float32)
+    ref = None
+    for env in ({"PICP_VO_FUSE": "0", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
+                {"PICP_VO_FUSE": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
+                {"PICP_VO_FUSE": None, "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None}):
+        for k, v in env.items():
+            if v is None:
+                monkeypatch.delenv(k, raising=False)
+            else:
+                monkeypatch.setenv(k, v)
+        outs = _vo_outputs(native, F, s.K, first, steps, boot)
+        if ref is None:
+            ref = outs[0]
+            assert min(int(r["n_corr"][1:].min()) for r in ref[1]) > 0
+        for o in outs:
+            _assert_same_bits(ref, o, str(env))
+
+
 def test_block_batch_beside_vo_bit_identical(native, monkeypatch):
     """A block-mode batch (the C4/C5 kernel) solved on its own stream while a VO sequence runs
     its matcher (MFMA) and step kernels beside it gives the bits of its solo run, every rep."""
