@@ -612,8 +612,13 @@ __device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, fl
     auto run = [&](auto rcp) {
 #pragma unroll
       for (int k = 0; k < NPT; ++k)
-        accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, decltype(rcp)::value>(T, C, thr, inv_thr, xs[k], ys[k], zs[k],
-                                                                           us[k], vs[k], first + k * stride < n, a, cnt);
+        // the last slot only in waves that hold an item there (a wave-uniform branch): a frame
+        // that fills 3.5 of 4 slots leaves whole waves empty in it, and with waves dealt to the
+        // SIMDs in turn every SIMD then issues one slot less when n <= (NPT - 1/2) x BS (C5's
+        // ~1,750 correspondences on 2,048 slots).  A skipped item adds exact zeros: same bits.
+        if (NPT < 2 || k + 1 < NPT || __any(first + k * stride < n))
+          accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, decltype(rcp)::value>(T, C, thr, inv_thr, xs[k], ys[k], zs[k],
+                                                                             us[k], vs[k], first + k * stride < n, a, cnt);
     };
     if (__all(fast))
       run(std::integral_constant<int, RCP_FAST>());
