@@ -7,7 +7,8 @@
 //   new    = add_new_world_points(corr, pairs)                (src/my_utilities.cpp:413-434)
 //   map   += triangulatePoints(prev pose, pose, new)          (src/cam.cpp:94-140)
 // Here every frame of a segment is one STEP and all segments of a sequence advance together:
-// one step = 4 launches over all segments (world match, gather, picp_block_kernel, append),
+// one step = 3 launches over all segments (world match, picp_block_kernel with the gather fused
+// in -- picp_block.hip vo_gather_items; 4 with PICP_VO_FUSE=0 -- and append),
 // with every count (map size, correspondences, new points) living in device memory, so a
 // whole sequence is enqueued (and hipGraph-captured) without a single host round trip.
 //
