@@ -571,20 +571,35 @@ static hipError_t vo_enqueue(picp_vo* h) {
   const bool fused = h->fuse && picp_vo_block_fusable(h->npt, h->max_obs);
 #endif
   if (e == hipSuccess && C > 1) e = hipEventRecord(h->ev_cj[0], h->stream);  // fork
-  for (int c = 0; c < C && e == hipSuccess; ++c) {
-    hipStream_t st = (c == 0) ? h->stream : h->cstream[c];
+  // the chains' launches are enqueued step by step, chain after chain within a step: enqueued
+  // chain after chain, every later chain's first launch waited on the host for the earlier
+  // chains' whole sequence (~120 launches each), which is how long the GPU ran without it at the
+  // start of a timed region.  Each stream's own order, and so every result, is unchanged.
+  std::vector<hipStream_t> cst((size_t)C);
+  std::vector<VoArgs> cv((size_t)C, h->vargs);
+  std::vector<int> csteps((size_t)C, 0);
+  int max_steps = 0;
+  for (int c = 0; c < C; ++c) {
+    cst[c] = (c == 0) ? h->stream : h->cstream[c];
     const int s0 = (int)((int64_t)h->n_seg * c / C), s1 = (int)((int64_t)h->n_seg * (c + 1) / C);
-    VoArgs V = h->vargs;
-    V.seg0 = s0;
-    V.n_seg = s1 - s0;
-    int steps = 0;
-    for (int s = s0; s < s1; ++s) steps = std::max(steps, (int)h->segs[s].steps);
-    if (c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
-    for (int t = 0; t < steps && e == hipSuccess; ++t) {
-      if (!(skip & 8))
-      e = picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
-                                 V.map_n1, V.map_n2, h->wprobs_d + s0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
-                                 h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
+    cv[c].seg0 = s0;
+    cv[c].n_seg = s1 - s0;
+    for (int s = s0; s < s1; ++s) csteps[c] = std::max(csteps[c], (int)h->segs[s].steps);
+    max_steps = std::max(max_steps, csteps[c]);
+  }
+  for (int t = 0; t < max_steps && e == hipSuccess; ++t) {
+    for (int c = 0; c < C && e == hipSuccess; ++c) {
+      if (t >= csteps[c]) continue;
+      hipStream_t st = cst[c];
+      const VoArgs& V = cv[c];
+      const int s0 = V.seg0, s1 = V.seg0 + V.n_seg;
+      (void)s1;
+      // chain c starts after chain c-1's first world match (enqueued just before, at t = 0)
+      if (t == 0 && c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
+      if (e == hipSuccess && !(skip & 8))
+        e = picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
+                                   V.map_n1, V.map_n2, h->wprobs_d + s0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
+                                   h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
       if (fused) {
         if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs);
@@ -601,8 +616,8 @@ static hipError_t vo_enqueue(picp_vo* h) {
       if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
       if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
     }
-    if (e == hipSuccess && c > 0) e = hipEventRecord(h->ev_cj[c], st);
   }
+  for (int c = 1; c < C && e == hipSuccess; ++c) e = hipEventRecord(h->ev_cj[c], cst[c]);
   for (int c = 1; c < C && e == hipSuccess; ++c) e = hipStreamWaitEvent(h->stream, h->ev_cj[c], 0);  // join
   return e;
 }
