@@ -539,7 +539,8 @@ def bench_vo(args, rk, torch):
     """C5: the whole sequence is split into contiguous segments of --seg-len PICP steps (one-frame
     overlap); ranks take contiguous ranges of segments (strong scaling: the
     sequence is fixed).  One step = one run of this rank's segments (pair matching of all its
-    frames, bootstrap, then per frame: world match, gather, PICP block kernel, triangulate/append).
+    frames, bootstrap, then per frame: world match, PICP block kernel with the gather fused in,
+    triangulate/append).
     value = frames estimated by all ranks / max-over-ranks time."""
     import numpy as np
     import picp_amd
