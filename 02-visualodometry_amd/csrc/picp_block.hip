@@ -47,13 +47,25 @@ using namespace picp;
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
 
 // Diagnostic build only (-DPICP_STAMPS): s_memrealtime per phase of rounds 11 and 12 seen by
-// thread 0 of blocks < 256 (tools/bstamps.py).
+// thread 0 of blocks < 1024, and where each block ran (words 7, 8: HW_REG_XCC_ID, HW_REG_HW_ID)
+// (tools/bstamps.py).
 #ifdef PICP_STAMPS
-__device__ unsigned long long picp_bstamps[2][256][8];
+#define PICP_BSTAMP_BLOCKS 1024
+__device__ unsigned long long picp_bstamps[2][PICP_BSTAMP_BLOCKS][10];
 #define BSTAMP(k)                                                                               \
   do {                                                                                          \
-    if (threadIdx.x == 0 && (round == 11 || round == 12) && blockIdx.x < 256)                    \
+    if (threadIdx.x == 0 && (round == 11 || round == 12) && blockIdx.x < PICP_BSTAMP_BLOCKS)     \
       picp_bstamps[round - 11][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                \
+  } while (0)
+#define BSTAMP_PLACE()                                                                          \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < PICP_BSTAMP_BLOCKS) {                                   \
+      unsigned xcc, hwid;                                                                       \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                       \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));                       \
+      picp_bstamps[0][blockIdx.x][7] = picp_bstamps[1][blockIdx.x][7] = xcc;                    \
+      picp_bstamps[0][blockIdx.x][8] = picp_bstamps[1][blockIdx.x][8] = hwid;                   \
+    }                                                                                           \
   } while (0)
 extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words) {
   const size_t cap = sizeof(picp_bstamps) / sizeof(unsigned long long);
@@ -61,50 +73,8 @@ extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words
                              hipMemcpyDeviceToHost);
 }
 #else
-#define BSTAMP(k) \
-  do {            \
-  } while (0)
-#endif
-
-// Diagnostic build only (-DPICP_BDIAG, tools/bdiag_check.py, tools/bdiag_vo.py): per (problem,
-// round), the pose each wave linearized at, the 8 wave sums of every term, the converted totals,
-// the finishing wave's new pose, a lane-agreement count of the finishing wave, per wave the lanes
-// whose permlane/DPP reduction differs from the ds_bpermute form of the same sums, and an XOR
-// checksum of the problem's inputs.  Batch mode: a uniform split-1 batch of picp_bdiag_nprob
-// problems, record (problem, round).  VO mode (picp_bdiag_cap > 0): the sequence's launches,
-// record (segment = offset / cap, launch count of that segment, round).
-#ifdef PICP_BDIAG
-#ifndef PICP_BDIAG_PARTS
-#define PICP_BDIAG_PARTS 15  // 1 input checksum, 2 wave poses, 4 wave sums + totals, 8 finish
-#endif
-#define BDIAG_REC 576  // [448 + 50 j]: finish of lane 0 (j 0) / lane 48 (j 1): 32 totals, dx, R t;
-                       // [416 + 2w]: lanes of wave w whose pose differs from lane 0's; [432]: same, finish;
-                       // [434..439]: finish inputs that differ from lane 0's: s_tot words, pose, chi_prev
-__device__ float* picp_bdiag_buf;
-__device__ int picp_bdiag_nprob;
-__device__ int picp_bdiag_rounds;
-__device__ long long picp_bdiag_cap;
-__device__ int picp_bdiag_nseg;
-__device__ int picp_bdiag_steps;
-__device__ unsigned picp_bdiag_cnt[4096];
-__device__ float* picp_bdiag_lane;  // part 16: VO step 0, [segment][round][wave][lane][32] folded partials
-extern "C" hipError_t picp_debug_bdiag_lane(float* buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_lane), &buf, sizeof(buf));
-}
-extern "C" hipError_t picp_debug_bdiag_set(float* buf, int n_problems, int rounds, long long cap, int nseg,
-                                           int steps) {
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_buf), &buf, sizeof(buf));
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_nprob), &n_problems, sizeof(int));
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_rounds), &rounds, sizeof(int));
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_cap), &cap, sizeof(cap));
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_nseg), &nseg, sizeof(int));
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_steps), &steps, sizeof(int));
-  static const unsigned zero[4096] = {};
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(picp_bdiag_cnt), zero, sizeof(zero));
-  return e;
-}
-#define BDIAG_ON (s_diag != nullptr && round <= picp_bdiag_rounds)
-#define BDIAG_PTR (s_diag + (size_t)(round - 1) * BDIAG_REC)
+#define BSTAMP(k) ((void)0)
+#define BSTAMP_PLACE() ((void)0)
 #endif
 
 // The VO step's gather fused into the block kernel (VoT = VoArgs; the separate kernel is
@@ -215,9 +185,9 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
         us[kk] = s_sl[3][o];
         vs[kk] = s_sl[4][o];
       }
-    if (q == qlast) {
+    if (q == qlast) {  // no item at all (n == 0): zeros, never the slice's unwritten words
 #pragma unroll
-      for (int v = 0; v < 5; ++v) lastv[v] = s_sl[v][last - q * VOG_SLICE];
+      for (int v = 0; v < 5; ++v) lastv[v] = (n > 0) ? s_sl[v][last - q * VOG_SLICE] : 0.0f;
     }
     __syncthreads();
   }
@@ -241,8 +211,21 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
   return n;
 }
 
-template <int NPT, int PH, int BS, typename VoT = NoVo>
-__global__ __launch_bounds__(BS, 2) void picp_block_kernel(
+// Issue priority of a block's waves by phase (-DPICP_BPRIO, A/B): the round's tail (the wave
+// reduction, the combine and partner exchange, the one-wave solve) is a dependency chain; when a
+// second block shares the CU (split 4), its linearize would take the SIMDs' issue slots ahead of it.
+#ifdef PICP_BPRIO
+#define BPRIO_TAIL() __builtin_amdgcn_s_setprio(3)
+#define BPRIO_LIN() __builtin_amdgcn_s_setprio(0)
+#else
+#define BPRIO_TAIL() ((void)0)
+#define BPRIO_LIN() ((void)0)
+#endif
+
+// MINW: waves per SIMD the register budget must allow (2: <= 256 VGPRs, one 512-thread block per
+// CU; 4: <= 128 VGPRs, two 512-thread blocks per CU -- split 4's layout)
+template <int NPT, int PH, int BS, typename VoT = NoVo, int MINW = 2>
+__global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpProblem* __restrict__ probs, const PicpState* __restrict__ st_in,
@@ -251,6 +234,7 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     const VoT vo, int vo_t) {
   constexpr bool VOG = std::is_same<VoT, VoArgs>::value;  // the VO step's gather fused in
   PICP_KFENCE_IN();
+  BSTAMP_PLACE();
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   // wave sums, term-major: the lane combining term e reads its BS/64 wave sums as 16-B loads
   __shared__ __attribute__((aligned(16))) float s_wave[PICP_NPART][BS / 64];
@@ -286,27 +270,6 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     n = min(n, first + part) - first;
     if (n > 0) base += first;  // an empty part keeps a valid base (its loads are clamped to it)
   }
-#ifdef PICP_BDIAG
-  __shared__ float* s_diag;
-  __shared__ float* s_ldiag;
-  if (tid == 0) {
-    float* d = nullptr;
-    s_ldiag = nullptr;
-    if (picp_bdiag_buf && split == 1) {
-      if (picp_bdiag_cap > 0 && !A.uniform) {
-        const long long seg = base / picp_bdiag_cap;
-        const unsigned k = atomicAdd(&picp_bdiag_cnt[seg & 4095], 1u);
-        if (seg < picp_bdiag_nseg && (int)k < picp_bdiag_steps)
-          d = picp_bdiag_buf + ((size_t)seg * picp_bdiag_steps + k) * picp_bdiag_rounds * BDIAG_REC;
-        if (seg < picp_bdiag_nseg && k == 0 && picp_bdiag_lane)
-          s_ldiag = picp_bdiag_lane + (size_t)seg * picp_bdiag_rounds * BS * PICP_NPART;
-      } else if (picp_bdiag_cap == 0 && A.uniform && n_problems == picp_bdiag_nprob) {
-        d = picp_bdiag_buf + (size_t)p * picp_bdiag_rounds * BDIAG_REC;
-      }
-    }
-    s_diag = d;
-  }
-#endif
   bgu64_t* const xgg = (bgu64_t*)xg;
   // split: exchange tags are tbase + round, tbase = the rounds this grid slot ran in earlier
   // launches on these buffers (partners run identical solves, so their bases stay equal); stale
@@ -366,17 +329,6 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     s_st = s;
   }
   __syncthreads();
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 1)
-  if (s_diag) {  // XOR of the bits of every input item (order-free), and n
-    unsigned x = 0;
-    for (int i = tid; i < n; i += BS)
-      x ^= __float_as_uint(X[base + i]) ^ (__float_as_uint(Y[base + i]) * 3u) ^ (__float_as_uint(Z[base + i]) * 5u) ^
-           (__float_as_uint(U[base + i]) * 7u) ^ (__float_as_uint(V[base + i]) * 11u);
-    for (int o = 32; o > 0; o >>= 1) x ^= (unsigned)__shfl_xor((int)x, o);
-    if (lane == 0) atomicXor(reinterpret_cast<unsigned*>(s_diag + 413), x);
-    if (tid == 0) s_diag[414] = (float)n;
-  }
-#endif
 
   Cam C;
   C.k00 = A.K[0]; C.k10 = A.K[1]; C.k20 = A.K[2];
@@ -393,32 +345,12 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
   float chi_prev = FLT_MAX;  // exec/icp_test.cpp:89
   for (int round = 1; !s_done; ++round) {
     BSTAMP(0);
+    BPRIO_LIN();
     Pose T;
     T.r00 = s_pose[0]; T.r10 = s_pose[1]; T.r20 = s_pose[2];
     T.r01 = s_pose[3]; T.r11 = s_pose[4]; T.r21 = s_pose[5];
     T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 32)
-    if (BDIAG_ON) {  // lanes whose pose differs from lane 0's (the pose every lane linearizes at)
-      const float tv[12] = {T.r00, T.r10, T.r20, T.r01, T.r11, T.r21, T.r02, T.r12, T.r22, T.t0, T.t1, T.t2};
-      bool mism = false;
-#pragma unroll
-      for (int i = 0; i < 12; ++i)
-        mism |= __float_as_int(tv[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(tv[i]));
-      const unsigned long long mm = __ballot(mism);
-      if (lane == 0 && mm) {
-        BDIAG_PTR[416 + 2 * wave] = __uint_as_float((unsigned)mm);
-        BDIAG_PTR[417 + 2 * wave] = __uint_as_float((unsigned)(mm >> 32));
-      }
-    }
-#endif
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 2)
-    if (BDIAG_ON && lane == 0) {
-      float* d = BDIAG_PTR + wave * 12;
-      d[0] = T.r00; d[1] = T.r10; d[2] = T.r20; d[3] = T.r01; d[4] = T.r11; d[5] = T.r21;
-      d[6] = T.r02; d[7] = T.r12; d[8] = T.r22; d[9] = T.t0; d[10] = T.t1; d[11] = T.t2;
-    }
-#endif
     // accumulation form by register-resident items per lane (picp_device.h acc_pairs): two slots
     // for NPT 8, one slot below
     float v[PICP_NPART];
@@ -457,26 +389,8 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       BSTAMP(1);
       acc_fold(a, v);
     }
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 16)
-    if (s_ldiag && round <= picp_bdiag_rounds) {
-      float* d = s_ldiag + ((size_t)(round - 1) * BS + tid) * PICP_NPART;
-#pragma unroll
-      for (int i = 0; i < PICP_NPART; ++i) d[i] = v[i];
-    }
-#endif
-#if defined(PICP_BDIAG) && !defined(PICP_BDIAG_NOCHK)
-    float vchk[PICP_NPART];
-#pragma unroll
-    for (int i = 0; i < PICP_NPART; ++i) vchk[i] = v[i];
-    const float rchk = wave_reduce32_bperm(vchk, lane);
-#endif
+    BPRIO_TAIL();
     const float wred = wave_reduce32(v, lane);
-#if defined(PICP_BDIAG) && !defined(PICP_BDIAG_NOCHK)
-    {
-      const int nbad = __popcll(__ballot(__float_as_int(rchk) != __float_as_int(wred)));
-      if (BDIAG_ON && lane == 0) BDIAG_PTR[405 + wave] = (float)nbad;
-    }
-#endif
     const float wsum = wave_counts(wred, lane, (Cnt){nr.n_in + nd.n_in, nr.n_proj + nd.n_proj});
     if ((lane & 1) == 0) s_wave[lane >> 1][wave] = wsum;
     BSTAMP(2);
@@ -494,10 +408,6 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
       float ws[BS / 64];  // every load issued before the first add (one LDS wait)
 #pragma unroll
       for (int w = 0; w < BS / 64; ++w) ws[w] = s_wave[tid][w];
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 4)
-      if (BDIAG_ON && BS == 512)
-        for (int w = 0; w < 8; ++w) BDIAG_PTR[96 + tid * 8 + w] = ws[w];
-#endif
       double t = (double)ws[0];
 #pragma unroll
       for (int w = 1; w < BS / 64; ++w) t += (double)ws[w];
@@ -548,9 +458,6 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
           if (q < split) t += part_t[q];
       }
       s_tot[tid] = total_word(A, tid, t);  // lane e converts total e
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 4)
-      if (BDIAG_ON) BDIAG_PTR[352 + tid] = total_word(A, tid, t);
-#endif
     }
     // the totals (and s_tmo) were written by lanes < 32 of wave 0, which also runs the solve:
     // a wave barrier orders them, the other waves wait at the block barrier after the solve
@@ -562,100 +469,8 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
     BSTAMP(4);
     if (wave == 0) {  // the wave finishes the round (every lane the same values, state in registers)
       RoundOut o;
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 64)
-      if (BDIAG_ON) {  // which finish inputs differ across the wave's lanes
-        bool m_tot = false, m_pose = false;
-#pragma unroll
-        for (int i = 0; i < PICP_NPART; ++i) {
-          const float x = s_tot[i];
-          m_tot |= __float_as_int(x) != __builtin_amdgcn_readfirstlane(__float_as_int(x));
-        }
-#pragma unroll
-        for (int i = 0; i < 9; ++i) m_pose |= __float_as_int(pr[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pr[i]));
-#pragma unroll
-        for (int i = 0; i < 3; ++i) m_pose |= __float_as_int(pt[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pt[i]));
-        const bool m_chi = __float_as_int(chi_prev) != __builtin_amdgcn_readfirstlane(__float_as_int(chi_prev));
-        const unsigned long long a = __ballot(m_tot), b = __ballot(m_pose), c = __ballot(m_chi);
-        if (lane == 0 && (a | b | c)) {
-          float* d = BDIAG_PTR;
-          d[434] = __uint_as_float((unsigned)a); d[435] = __uint_as_float((unsigned)(a >> 32));
-          d[436] = __uint_as_float((unsigned)b); d[437] = __uint_as_float((unsigned)(b >> 32));
-          d[438] = __uint_as_float((unsigned)c); d[439] = __uint_as_float((unsigned)(c >> 32));
-        }
-      }
-#endif
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 128)
-      {  // finish_round_pose restated with per-stage records of lanes 0 and 48
-        float twr[PICP_NPART];
-#pragma unroll
-        for (int i = 0; i < PICP_NPART; ++i) twr[i] = s_tot[i];
-        o.chi_in = twr[PICP_P_CHI_IN];
-        o.chi_out = twr[PICP_P_CHI_OUT];
-        o.n_in = __float_as_int(twr[PICP_P_N_IN]);
-        o.n_proj = __float_as_int(twr[PICP_P_N_PROJ]);
-        o.converged = 0;
-        float dx[6] = {0, 0, 0, 0, 0, 0};
-        if (o.n_in < A.min_inliers) {
-          o.ok = 0;
-          o.done = 1;
-        } else {
-          ldl6_solve(twr, dx);
-          apply_update(dx, pr, pt);
-          o.ok = 1;
-          o.done = 0;
-          const float prev = chi_prev, cur = o.chi_in;
-          const float rel = (prev > 1e-10f) ? fabsf(prev - cur) / prev : 0.0f;
-          if (rel < A.conv_eps) {
-            o.converged = 1;
-            o.done = 1;
-          } else {
-            chi_prev = cur;
-          }
-          if (round >= A.max_rounds) o.done = 1;
-        }
-        if (BDIAG_ON && (lane == 0 || lane == 48)) {
-          float* d = BDIAG_PTR + 448 + (lane == 48 ? 50 : 0);
-#pragma unroll
-          for (int i = 0; i < 32; ++i) d[i] = twr[i];
-#pragma unroll
-          for (int i = 0; i < 6; ++i) d[32 + i] = dx[i];
-#pragma unroll
-          for (int i = 0; i < 9; ++i) d[38 + i] = pr[i];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) d[47 + i] = pt[i];
-        }
-      }
-#else
       finish_round_pose<PICP_FINISH_WAVE>(A, s_tot, round, pr, pt, chi_prev, o);
-#endif
       if (s_tmo) o.done = 1;  // a partner wait timed out: stop (the host reports the error)
-#if defined(PICP_BDIAG) && (PICP_BDIAG_PARTS & 8)
-      if (BDIAG_ON) {
-        bool mism = false;
-#pragma unroll
-        for (int i = 0; i < 9; ++i)
-          mism |= __float_as_int(pr[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pr[i]));
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-          mism |= __float_as_int(pt[i]) != __builtin_amdgcn_readfirstlane(__float_as_int(pt[i]));
-        const unsigned long long mm = __ballot(mism);
-        const int nm = __popcll(mm);
-        if (lane == 0) {
-          float* d = BDIAG_PTR;
-          d[432] = __uint_as_float((unsigned)mm);
-          d[433] = __uint_as_float((unsigned)(mm >> 32));
-#pragma unroll
-          for (int i = 0; i < 9; ++i) d[384 + i] = pr[i];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) d[393 + i] = pt[i];
-          d[396] = o.chi_in;
-          d[397] = (float)o.n_in;
-          d[398] = (float)o.done;
-          d[399] = chi_prev;
-          d[404] = (float)nm;
-        }
-      }
-#endif
       if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];
@@ -679,40 +494,61 @@ __global__ __launch_bounds__(BS, 2) void picp_block_kernel(
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part (BS 512)
 
+// Threads per block of a split layout: 512 for split 1 and 2 (one block per CU); split 4 runs two
+// blocks per CU, either 256-thread blocks (one wave per SIMD each, <= 256 VGPRs) or 512-thread
+// blocks (two waves per SIMD each, <= 128 VGPRs: MINW 4).
+static int s4_bs() {
+  static const int bs = [] {
+    const char* e = getenv("PICP_BLOCK_S4BS");
+    return (e && atoi(e) == 256) ? 256 : 512;
+  }();
+  return bs;
+}
+extern "C" int picp_block_threads(int split) { return (split == 4) ? s4_bs() : PICP_BBLOCK; }
+
 // dynamic LDS of a launch: the part of a problem (or of its 1/split share) past the
 // register-resident npt x BS items, capped by the stage
 static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out) {
   const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
-  const int bs = (split == 4) ? 256 : PICP_BBLOCK;
+  const int bs = picp_block_threads(split);
   const int lds_cap = (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
   const int lds_items = (per_block > npt * bs) ? min(per_block - npt * bs, lds_cap) : 0;
   if (lds_items_out) *lds_items_out = lds_items;
   return (size_t)5 * lds_items * sizeof(float);
 }
 
-template <int N, int B>
-static const void* block_kernel_nb(int var) {
+// the kernel of a launch: (threads, waves per SIMD) = (512, 2), (256, 2) or split 4's (512, 4)
+template <int N, int B, int W>
+static const void* block_kernel_nbw(int var) {
   switch (var) {
-    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, B>;
-    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, B>;
-    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, B>;
+    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, B, NoVo, W>;
+    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, B, NoVo, W>;
+    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, B, NoVo, W>;
   }
 }
 
 template <int N>
-static const void* block_kernel_n(int var, int bs) {
-  return (bs == 256) ? block_kernel_nb<N, 256>(var) : block_kernel_nb<N, 512>(var);
+static const void* block_kernel_n(int var, int bs, int split) {
+  if (bs == 256) return block_kernel_nbw<N, 256, 2>(var);
+  if (split == 4) {
+    if constexpr (N <= 4) return block_kernel_nbw<N, 512, 4>(var);  // <= 128 VGPRs: NPT <= 4
+    return nullptr;
+  }
+  return block_kernel_nbw<N, 512, 2>(var);
 }
 
-static const void* block_kernel_ptr(int npt, int var, int bs) {
+static const void* block_kernel_ptr(int npt, int var, int bs, int split) {
   switch (npt) {
-    case 1: return block_kernel_n<1>(var, bs);
-    case 2: return block_kernel_n<2>(var, bs);
-    case 4: return block_kernel_n<4>(var, bs);
-    case 8: return block_kernel_n<8>(var, bs);
+    case 1: return block_kernel_n<1>(var, bs, split);
+    case 2: return block_kernel_n<2>(var, bs, split);
+    case 4: return block_kernel_n<4>(var, bs, split);
+    case 8: return block_kernel_n<8>(var, bs, split);
     default: return nullptr;
   }
 }
+
+// Register items per lane the split-4 512-thread layout allows (its 128-VGPR budget); 8 otherwise.
+extern "C" int picp_block_npt_cap(int split) { return (split == 4 && s4_bs() == 512) ? 4 : 8; }
 
 // Blocks of the variants a launch with these arguments may use that one CU holds at once (the
 // hardware limit from registers, LDS and waves; other work on the device is not counted; the
@@ -721,11 +557,11 @@ static const void* block_kernel_ptr(int npt, int var, int bs) {
 // the whole grid fits.
 extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu) {
   if (!blocks_per_cu || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
-  const int bs = (split == 4) ? 256 : PICP_BBLOCK;
+  const int bs = picp_block_threads(split);
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr);
   int best = -1;
   for (int keep = 0; keep < 2; ++keep) {
-    const void* fn = block_kernel_ptr(npt, picp_variant(K, keep), bs);
+    const void* fn = block_kernel_ptr(npt, picp_variant(K, keep), bs, split);
     if (!fn) return hipErrorInvalidValue;
     if (lds_bytes > 65536) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
@@ -742,9 +578,10 @@ extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const 
 
 // max_n: the largest problem of the launch (sizes the LDS stage: max_n/split - npt*BS items,
 // capped).  split = 1: grid = n_problems blocks of 512.  split = 2: grid = round_up(2 n_problems,
-// 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of 256, two
-// per CU; all co-resident (the caller checks the grid against the CUs), xg = 2 * grid * 64
-// u64 granules, tagbase = grid u32 tag bases (both zeroed once per layout), err the error word.
+// 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of
+// picp_block_threads(4), two per CU; all co-resident (the caller checks the grid against the
+// CUs), xg = 2 * grid * 64 u64 granules, tagbase = grid u32 tag bases (both zeroed once per
+// layout), err the error word.
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
@@ -756,39 +593,19 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
   if (split > 1 && (!xg || !err || !tagbase)) return hipErrorInvalidValue;
   const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
   const int var = picp_variant(args->K, args->keep_outliers);
-  const int bs = (split == 4) ? 256 : PICP_BBLOCK;
+  const int bs = picp_block_threads(split);
+  const void* fn = block_kernel_ptr(npt, var, bs, split);
+  if (!fn) return hipErrorInvalidValue;
   int lds_items = 0;
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, &lds_items);
-#define PICP_LAUNCH_B3(N, P, B)                                                                            \
-  {                                                                                                        \
-    if (lds_bytes > 65536)                                                                                 \
-      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, B>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                          (int)lds_bytes);                                                                 \
-    hipLaunchKernelGGL((picp_block_kernel<N, P, B>), dim3(grid), dim3(B), lds_bytes, stream, X, Y, Z, U, V, \
-                       *args, probs, st_in, st_out, lds_items, split, n_problems, xg, err, tagbase, timeout_ticks, \
-                       NoVo{}, 0);                                                                     \
-  }
-#define PICP_LAUNCH_BV(N, B)                                                              \
-  if (var == PICP_V_PINHOLE) PICP_LAUNCH_B3(N, PICP_V_PINHOLE, B)                           \
-  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_B3(N, PICP_V_PINHOLE_KEEP, B)            \
-  else PICP_LAUNCH_B3(N, PICP_V_GENERAL, B)
-#define PICP_LAUNCH_B(N)   \
-  if (bs == 256) {         \
-    PICP_LAUNCH_BV(N, 256) \
-  } else {                 \
-    PICP_LAUNCH_BV(N, 512) \
-  }
-  switch (npt) {
-    case 1: PICP_LAUNCH_B(1); break;
-    case 2: PICP_LAUNCH_B(2); break;
-    case 4: PICP_LAUNCH_B(4); break;
-    case 8: PICP_LAUNCH_B(8); break;
-    default: return hipErrorInvalidValue;
-  }
-#undef PICP_LAUNCH_B
-#undef PICP_LAUNCH_BV
-#undef PICP_LAUNCH_B3
-  return hipGetLastError();
+  if (lds_bytes > 65536) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  NoVo novo{};
+  int zero = 0;
+  void* kargs[] = {(void*)&X, (void*)&Y, (void*)&Z, (void*)&U, (void*)&V, (void*)args, (void*)&probs,
+                   (void*)&st_in, (void*)&st_out, (void*)&lds_items, (void*)&split, (void*)&n_problems,
+                   (void*)&xg, (void*)&err, (void*)&tagbase, (void*)&timeout_ticks, (void*)&novo, (void*)&zero};
+  hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(bs), kargs, lds_bytes, stream);
+  return (e != hipSuccess) ? e : hipGetLastError();
 }
 
 // The VO step's PICP with its gather fused in (vo_gather_items): segments a->seg0 .. + n_seg of

@@ -936,6 +936,9 @@ __device__ __forceinline__ void taylor_sincos(float a, float* s, float* c) {
 
 // src/defs.h:100-136 v2tEuler's rotation: Rd = Rx(a)*Ry(b)*Rz(c) (float) of dx[3..5].
 __device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3]) {
+  // every product rounded before its sum, whatever code surrounds the inlined update: the
+  // compiler may not choose which of a*b + c*d to fuse
+#pragma clang fp contract(off)
   float sa, ca, sb, cb, sc, cc;
   if (fabsf(dx[3]) <= 0.0625f && fabsf(dx[4]) <= 0.0625f && fabsf(dx[5]) <= 0.0625f) {
     taylor_sincos(dx[3], &sa, &ca);
@@ -963,6 +966,7 @@ __device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3
 // src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
 // src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
 __device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
+#pragma clang fp contract(off)  // products rounded, then summed in order (as the oracle)
   float Rd[3][3];
   update_rotation(dx, Rd);
   float Rn[9], tn[3];

@@ -42,7 +42,17 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
                                         unsigned int* tagbase, unsigned long long timeout_ticks);
+extern "C" hipError_t picp_launch_pair(hipStream_t stream, int n_problems, int npt, const float* X, const float* Y,
+                                       const float* Z, const float* U, const float* V, const PicpArgs* args,
+                                       const PicpState* st_in, PicpState* st_out, int max_n, int split,
+                                       unsigned long long* xg, unsigned int* err, unsigned int* tagbase,
+                                       unsigned long long timeout_ticks);
+extern "C" hipError_t picp_pair_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu);
+extern "C" int picp_pair_grid(int n_problems, int split);
+extern "C" int picp_pair_npt_cap(void);
 extern "C" int picp_block_max_items(void);
+extern "C" int picp_block_threads(int split);
+extern "C" int picp_block_npt_cap(int split);
 extern "C" int picp_persistent_block(void);
 extern "C" hipError_t picp_persistent_occupancy(int npt, const float K[9], int* blocks_per_cu);
 extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu);
@@ -187,6 +197,7 @@ struct picp_batch {
   int64_t stride_u = 0;
   int num_cu = 256;            // compute units of the device
   int split = 1;               // block mode: blocks per problem (1, or 2 when 2*np fits the chip)
+  int pair = 0;                // block mode: two problems per block, rounds interleaved (picp_pair.hip)
   int mode = PICP_MODE_GRAPH;  // PICP_MODE_GRAPH (launch per round) / PICP_MODE_PERSISTENT
   int npt = 1;                 // persistent: correspondences per lane held in registers
   unsigned char* sync = nullptr;   // persistent: [err 16 B | pose granules | partial granules | tag bases]
@@ -216,7 +227,19 @@ struct picp_batch {
 // persistent launches and split block launches hand off through granules and report a timed-out
 // wait in the error word at the head of b->sync
 static bool uses_err_word(const picp_batch* b) {
-  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1);
+  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && (b->split > 1 || b->pair));
+}
+
+// exchange granules / tag bases of a split block layout: (grid, granule sets per block)
+static void xg_layout(const picp_batch* b, int64_t* grid, int64_t* sets) {
+  const int64_t ss = std::max(b->split, 1);
+  if (b->pair) {
+    *grid = picp_pair_grid((int)b->np, (int)ss);
+    *sets = 2;
+  } else {
+    *grid = ((ss * b->np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
+    *sets = 1;
+  }
 }
 
 static void drop_graph(picp_batch* b) {
@@ -367,8 +390,8 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
       // occupancy query says the whole grid is resident at once
       while (split > 1) {
         const int64_t part = round_up((max_n + split - 1) / split, 4);
-        const int bs = (split == 4) ? 256 : 512;
-        int cap = picp_block_max_items() / 512;
+        const int bs = picp_block_threads(split);
+        int cap = std::min(picp_block_max_items() / 512, picp_block_npt_cap(split));
         if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
         int snpt = 1;
         while (snpt < cap && (int64_t)snpt * bs < part) snpt *= 2;
@@ -382,18 +405,60 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
       b->split = split;
       if (split > 1) {  // register items per lane for a part
         const int64_t part = round_up((max_n + split - 1) / split, 4);
-        const int bs = (split == 4) ? 256 : 512;
-        int cap = picp_block_max_items() / 512;
+        const int bs = picp_block_threads(split);
+        int cap = std::min(picp_block_max_items() / 512, picp_block_npt_cap(split));
         if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
         bnpt = 1;
         while (bnpt < cap && (int64_t)bnpt * bs < part) bnpt *= 2;
       }
       b->npt = bnpt;
+      // pair mode (picp_pair.hip): two problems per block, one problem's serial round tail under
+      // the other's linearize (uniform batches).  The widest split whose grid is one block per
+      // CU; more pairs than CUs take split 1, which has no cross-block waits.
+      // PICP_BLOCK_PAIR=0|1 forces it off / on.
+      b->pair = 0;
+      {
+        int want = 0;
+        if (const char* e = getenv("PICP_BLOCK_PAIR")) want = atoi(e) != 0;
+        if (want && b->uniform && np >= 2 && !b->no_handoff) {
+          int ps = 1;
+          for (int S : {4, 2}) {
+            if (picp_pair_grid(np, S) <= b->num_cu && max_n >= 1024 * S) {
+              ps = S;
+              break;
+            }
+          }
+          if (const char* e = getenv("PICP_BLOCK_SPLIT")) {
+            const int v = atoi(e);
+            if (v == 1 || ((v == 2 || v == 4) && picp_pair_grid(np, v) <= b->num_cu)) ps = v;
+          }
+          const int64_t part = round_up((max_n + ps - 1) / ps, 4);
+          int cap = picp_pair_npt_cap();
+          if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
+          int pnpt2 = 1;
+          while (pnpt2 < cap && (int64_t)pnpt2 * 512 < part) pnpt2 *= 2;
+          bool ok = true;
+          if (ps > 1) {  // its blocks wait on each other: all of them resident at once
+            int occ = 0;
+            const int res = resident_per_cu(picp_pair_occupancy(pnpt2, ps, (int)max_n, b->K, &occ), occ) * b->num_cu;
+            ok = picp_pair_grid(np, ps) <= res;
+            if (ok) {
+              b->handoff_grid = picp_pair_grid(np, ps);
+              b->handoff_resident = res;
+            }
+          }
+          if (ok) {
+            b->pair = 1;
+            b->split = ps;
+            b->npt = pnpt2;
+          }
+        }
+      }
     }
   }
   // report the hand-off grid of the layout in use only (a candidate the occupancy check rejected
   // leaves no hand-off behind: picp_batch_residency then reads 0/0)
-  if (!(b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1))) {
+  if (!(b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1))) {  // pair split 1: none
     b->handoff_grid = 0;
     b->handoff_resident = 0;
   }
@@ -450,15 +515,16 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
     HIP_TRY(hipHostMalloc((void**)&b->st_pinned, (size_t)np * sizeof(PicpState), hipHostMallocDefault));
     b->np_cap = np;
   }
-  if (b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1)) {
+  if (uses_err_word(b)) {
     // persistent: error word | pose granules | partial granules (x2 parities);
-    // split block: error word | exchange granules (x2 parities, 64 per block)
-    const int64_t ss = std::max(b->split, 1);
-    const int64_t sgrid = ((ss * np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
+    // split block: error word | exchange granules (x2 parities, 64 per block and problem held)
+    // | tag bases
+    int64_t sgrid = 0, sets = 1;
+    xg_layout(b, &sgrid, &sets);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
                         ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
                                                (int64_t)np * 4, 256)
-                        : (size_t)round_up(16 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
+                        : (size_t)round_up(16 + 2 * sgrid * sets * 64 * 8 + sgrid * sets * 4, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
       b->sync = nullptr;
@@ -583,13 +649,16 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
     unsigned int* err = nullptr;
     unsigned long long* xg = nullptr;
     unsigned int* tagbase = nullptr;
-    if (b->split > 1) {  // tags continue from the per-slot tag bases: no memset per launch
-      const int64_t ss = b->split;
-      const int64_t sgrid = ((ss * b->np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
+    if (b->split > 1 || b->pair) {  // tags continue from the per-slot tag bases: no memset per launch
+      int64_t sgrid = 0, sets = 1;
+      xg_layout(b, &sgrid, &sets);
       err = reinterpret_cast<unsigned int*>(b->sync);
       xg = reinterpret_cast<unsigned long long*>(b->sync + 16);
-      tagbase = reinterpret_cast<unsigned int*>(xg + 2 * sgrid * 64);
+      tagbase = reinterpret_cast<unsigned int*>(xg + 2 * sgrid * sets * 64);
     }
+    if (b->pair)
+      return picp_launch_pair(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args, b->init_d,
+                              b->st_d[0], (int)b->max_n, b->split, xg, err, tagbase, b->timeout_ticks);
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
                              b->probs_d, b->init_d, b->st_d[0], (int)b->max_n, b->split, xg, err, tagbase,
                              b->timeout_ticks);

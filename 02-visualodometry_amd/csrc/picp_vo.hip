@@ -355,3 +355,13 @@ extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a,
   hipLaunchKernelGGL(vo_append_kernel, dim3(a->n_seg), dim3(VOA_BLOCK), 0, stream, *a, t);
   return hipGetLastError();
 }
+
+// 1 when this library's device code was built with packed FP32 (make PK=1, A/B builds only): the
+// VO runtime then defaults to the serial schedule
+extern "C" int picp_build_packed_fp32(void) {
+#ifdef PICP_ALLOW_PK
+  return 1;
+#else
+  return 0;
+#endif
+}

@@ -10,6 +10,7 @@
 // replayed by every later run.  No host round trip inside a run; no host fallback.
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -39,6 +40,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         unsigned int* tagbase, unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
 extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs);
+extern "C" int picp_build_packed_fp32(void);
 extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
                                            const PicpArgs* args, int64_t max_obs);
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
@@ -222,6 +224,14 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
     h->graph_env = true;
   }
   if (const char* e = getenv("PICP_VO_MATCH_FULL")) h->accept_only = atoi(e) != 0 ? 0 : 1;
+  // A/B libraries built with packed FP32 (make PK=1): their concurrent schedules are not
+  // bit-stable, so such a build defaults to the serial order and says so
+  if (picp_build_packed_fp32()) {
+    h->overlap = false;
+    h->chains = 1;
+    fprintf(stderr, "picp_vo_create: this library was built with packed FP32 (make PK=1, an A/B build): the "
+                    "VO schedule defaults to the serial order; concurrent schedules are not bit-stable with it\n");
+  }
   if (const char* e = getenv("PICP_VO_OVERLAP")) h->overlap = atoi(e) != 0;
   // at most two groups: three and four measured slower (C5 592k / 404k vs 597-600k frames/s with
   // two, round 2)
@@ -305,6 +315,39 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   CHECK_ARG(n_seg >= 1 && n_seg <= VO_MAX_GRID_Y, "picp_vo_set_segments: n_seg must be in [1, 65535]");
   CHECK_ARG(prm->max_rounds >= 0 && prm->max_rounds <= 100000, "params.max_rounds out of range");
   CHECK_ARG(!(prm->threshold != prm->threshold), "params.threshold is NaN");
+  // every argument is validated before the handle's current segments are released: a rejected
+  // call leaves the handle as it was
+  for (int s = 0; s < n_seg; ++s)
+    CHECK_ARG(steps[s] >= 1 && first[s] >= 0 && first[s] + steps[s] < h->n_frames,
+              "picp_vo_set_segments: segment out of range (needs frames first .. first+steps, steps >= 1)");
+  // The world match writes its outputs (wm_*) at the query frame's observation offsets.  Step t of
+  // segment s queries frame first[s] + t + 1, so two segments query one frame at the same step
+  // exactly when their first frames are equal: they would write the same rows in one launch, and
+  // that layout is rejected.  Segments querying one frame at different steps are fine in one step
+  // chain (the launches are ordered) but not across chains (PICP_VO_CHAINS=2 runs the groups'
+  // world matches concurrently), so such a layout runs the serial order.
+  {
+    std::vector<int64_t> f0s(first, first + n_seg);
+    std::sort(f0s.begin(), f0s.end());
+    for (int s = 1; s < n_seg; ++s)
+      if (f0s[s] == f0s[s - 1])
+        return picp_set_err(PICP_ERR_ARG, "picp_vo_set_segments: two segments start at frame %lld (they would "
+                            "query frame %lld at the same step)", (long long)f0s[s], (long long)f0s[s] + 1);
+  }
+  int chains_eff = std::min(h->chains, n_seg);
+  {
+    std::vector<int> q_group((size_t)h->n_frames, -1);
+    const int C = chains_eff;
+    for (int s = 0; s < n_seg; ++s) {
+      int grp = 0;
+      while (grp + 1 < C && s >= (int)((int64_t)n_seg * (grp + 1) / C)) ++grp;
+      for (int t = 0; t < steps[s]; ++t) {
+        const int64_t f = first[s] + t + 1;
+        if (q_group[f] >= 0 && q_group[f] != grp) chains_eff = 1;
+        q_group[f] = grp;
+      }
+    }
+  }
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipStreamSynchronize(h->stream));
   vo_free_segments(h);
@@ -313,8 +356,6 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   int64_t map_slots = 0, n_slots = 0;
   int max_steps = 0;
   for (int s = 0; s < n_seg; ++s) {
-    CHECK_ARG(steps[s] >= 1 && first[s] >= 0 && first[s] + steps[s] < h->n_frames,
-              "picp_vo_set_segments: segment out of range (needs frames first .. first+steps, steps >= 1)");
     VoSegment& G = segs[s];
     G.f0 = first[s];
     G.steps = steps[s];
@@ -327,29 +368,6 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     n_slots += G.steps + 1;
     max_steps = std::max(max_steps, (int)G.steps);
     for (int64_t f = G.f0; f < G.f0 + G.steps; ++f) is_curr[f] = 1;
-  }
-  // The world match writes its outputs (wm_*) at the query frame's observation offsets.  Two
-  // segments querying one frame at the same step would write the same rows in one launch, so
-  // that layout is rejected; segments querying one frame at different steps are fine in one step
-  // chain (the launches are ordered) but not across chains (PICP_VO_CHAINS=2 runs the groups'
-  // world matches concurrently), so such a layout runs the serial order.
-  int chains_eff = std::min(h->chains, n_seg);
-  {
-    std::vector<int> q_step((size_t)h->n_frames, -1), q_group((size_t)h->n_frames, -1);
-    const int C = chains_eff;
-    for (int s = 0; s < n_seg; ++s) {
-      int grp = 0;
-      while (grp + 1 < C && s >= (int)((int64_t)n_seg * (grp + 1) / C)) ++grp;
-      for (int t = 0; t < steps[s]; ++t) {
-        const int64_t f = first[s] + t + 1;
-        if (q_step[f] == t)
-          return picp_set_err(PICP_ERR_ARG, "picp_vo_set_segments: two segments query frame %lld at step %d",
-                              (long long)f, t);
-        if (q_group[f] >= 0 && q_group[f] != grp) chains_eff = 1;
-        q_step[f] = t;
-        q_group[f] = grp;
-      }
-    }
   }
   // frame->next problems grouped by step index: chunk k holds frame f0+k of every segment with
   // more than k steps (the bootstrap and step 0 read chunk 0, step t reads chunk t).  Frames of

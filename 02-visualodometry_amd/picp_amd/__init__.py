@@ -594,15 +594,16 @@ class VOSequence:
 
     def set_segments(self, first, steps, boot_poses, threshold=3000.0, **params):
         """boot_poses: (n_seg, 2, 4, 4) camera-in-world poses of frames first and first+1."""
-        self.first = np.ascontiguousarray(first, np.int64)
-        self.steps = np.ascontiguousarray(steps, np.int32)
-        B = np.asarray(boot_poses, np.float32).reshape(len(self.first), 2, 4, 4)
+        first = np.ascontiguousarray(first, np.int64)
+        steps = np.ascontiguousarray(steps, np.int32)
+        B = np.asarray(boot_poses, np.float32).reshape(len(first), 2, 4, 4)
         flat = np.ascontiguousarray(np.transpose(B, (0, 1, 3, 2)).reshape(-1))
         p = default_params(threshold=threshold, **params)
-        _check(lib().picp_vo_set_segments(self._h, len(self.first),
-                                          self.first.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-                                          self.steps.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+        _check(lib().picp_vo_set_segments(self._h, len(first), first.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                          steps.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                                           _fptr(flat), ctypes.byref(p)))
+        # a rejected call leaves the handle (and this view of it) unchanged
+        self.first, self.steps = first, steps
 
     def run(self):
         _check(lib().picp_vo_run(self._h))

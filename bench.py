@@ -313,7 +313,8 @@ def bench_frame(args, rk, torch):
     # the region is timed args.samples times and the median reported (median of >= 5)
     elapsed, (ev_ms, launch_us), el_all = _timed_samples(rk, torch, lambda: b.time(args.steps, **params),
                                                          args.samples)
-    err = rk.max([synth.se3_log_norm(b.poses()[0], T_gt[0])])[0]
+    T_gpu = b.poses()[0]
+    err = rk.max([synth.se3_log_norm(T_gpu, T_gt[0])])[0]
 
     info = b.info()
     default_cfg = (n == wl["n"] and R == 50)
@@ -376,7 +377,12 @@ def bench_frame(args, rk, torch):
     if args.workload == "c3" and not args.skip_extras and rk.world == 1:
         out["keep_outliers_true"] = _keep_outliers_leg(b, T_init, T_gt, params, args.steps)
     if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(xyz, uv, T_init[0], R, args.cpu_seconds)
+        out["cpu_baseline"], T_or = cpu_baseline(xyz, uv, T_init[0], R, args.cpu_seconds)
+        # parity of the timed frame: the GPU's pose after the timed solves vs the faithful oracle's
+        # solve of the same frame from the same prior (the cpu_baseline leg's last solve)
+        out["pose_err_vs_oracle_se3"] = synth.se3_log_norm(T_gpu, T_or)
+        out["pose_err_vs_oracle_note"] = ("SE(3) log norm, GPU %d-round solve vs the oracle's faithful float32 "
+                                          "restatement of the reference (north_star tolerance 1e-4)" % R)
         out["cpu_baseline_all_cores"] = cpu_baseline_mt(xyz, uv, T_init[0], R, max(2.0, args.cpu_seconds / 2))
     del b
     if args.workload == "c2" and not args.skip_extras:
@@ -390,6 +396,8 @@ def bench_frame(args, rk, torch):
         sub.n = sub.problems = sub.frames = sub.obs = 0
         out["c4"] = _compact(bench_c4(sub, rk, torch))
         if rk.world == 1:
+            out["c4"]["per_rank"], out["c4"]["projection"] = _c4_projection(sub, rk, torch, out["c4"]["value"])
+        if rk.world == 1:
             sub.workload = "c3"
             sub.skip_extras = True
             sub.cpu_seconds = 5.0
@@ -397,17 +405,39 @@ def bench_frame(args, rk, torch):
             c3["roofline"] = _resident_bound(c3["roofline"])
             out["c3"] = _compact(c3)
         out["c5"] = _compact(bench_vo(sub, rk, torch))
+        # SURVEY.md §8e's partition: 8 contiguous segments over the sequence (one per GPU of an
+        # 8-GPU node), each bootstrapped once; here all 8 run on this rank's GPU(s)
+        sub8 = argparse.Namespace(**vars(sub))
+        sub8.steps, sub8.warmup, sub8.samples = 2, 1, 3
+        F = args.frames or WORKLOADS["c5"]["frames"]
+        out["c5"]["partition_8e"] = _compact(bench_vo(sub8, rk, torch, seg_len=-(-(F - 1) // 8), tag="c5_8e"))
+        if rk.world == 1:
+            # the per-rank shape of the default partition at N = 8 (rank 0's 32 of the 250
+            # segments), on this GPU alone: each rank still runs every segment's dependent steps
+            n8 = bench_vo(sub, rk, torch, shard=(8, 0), tag="c5_n8")
+            total = out["c5"]["value"] * out["c5"]["ms_per_step"] * 1e-3  # frames per run
+            out["c5"]["per_rank_n8"] = _compact(n8)
+            out["c5"]["projection_n8"] = {
+                "projected_value": round(total / (n8["ms_per_step"] * 1e-3), 1),
+                "efficiency": round(total / (n8["ms_per_step"] * 1e-3) / (8 * out["c5"]["value"]), 4),
+                "basis": "the whole sequence's frames / the time of rank 0's share (32 of 250 segments) alone on one "
+                         "GPU: every rank still runs its segments' 40 dependent steps, so the time per run falls "
+                         "with the width of each step, not with the step count"}
     return out
 
 
 def _compact(d):
     keep = ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "timing", "roofline",
             "cpu_baseline", "cpu_baseline_all_cores",
-            "pose_err_vs_gt_se3", "pose_err_vs_gt_se3_max", "kernel_us", "kernel", "traffic", "traffic_source",
+            "pose_err_vs_gt_se3", "pose_err_vs_gt_se3_max", "pose_err_vs_oracle_se3", "pose_err_vs_oracle_note",
+            "pose_err_vs_oracle_se3_frame0", "trajectory", "chain_step_us", "per_rank", "projection",
+            "kernel_us", "kernel", "traffic", "traffic_source",
             "picp_iterations_per_s", "ranks", "config", "bootstrap")
     out = {k: d[k] for k in keep if k in d}
     if "config" in out:
-        out["config"] = {k: v for k, v in out["config"].items() if k in ("workload", "frames_total", "frames", "parallelism")}
+        out["config"] = {k: v for k, v in out["config"].items()
+                         if k in ("workload", "frames_total", "frames", "parallelism", "partition", "segments",
+                                  "segment_steps")}
     return out
 
 
@@ -446,10 +476,12 @@ def _keep_outliers_leg(b, T_init, T_gt, params, steps):
                     "by design (the reference's keep_outliers mode); parity with the oracle is tested"}
 
 
-def bench_c4(args, rk, torch):
+def bench_c4(args, rk, torch, shard=None):
     """C4: the fixed batch of 1024 frames x 10k split over the ranks (picp_shard_range); one step =
     one fused 50-round solve of this rank's frames; the timed region ends with the RCCL all-gather
-    of every frame's pose + stats to every rank (C-ABI picp_batch_allgather)."""
+    of every frame's pose + stats to every rank (C-ABI picp_batch_allgather).
+    shard=(world, rank): that rank's frames solved on this GPU alone (the per-rank shape of an
+    N-GPU run, no all-gather)."""
     import numpy as np
     import picp_amd
     from picp_amd import synth
@@ -457,7 +489,10 @@ def bench_c4(args, rk, torch):
     n = args.n or wl["n"]
     total = args.problems or wl["problems"]
     R = args.rounds
-    f0, f1 = picp_amd.shard_range(total, rk.world, rk.rank)
+    solo = shard is not None
+    if solo:
+        rk = _Solo()
+    f0, f1 = picp_amd.shard_range(total, *(shard if solo else (rk.world, rk.rank)))
     bt = synth.make_batch(f1 - f0, n, base_seed=1000, first=f0, outlier_frac=0.0, pixel_noise=0.5)
     b = picp_amd.Batch(bt["sizes"], device=rk.device)
     b.set_data(bt["xyz"], bt["uv"])
@@ -469,7 +504,7 @@ def bench_c4(args, rk, torch):
 
     def job():
         r = b.time(args.steps, **params)
-        if rk.comm is not None:
+        if getattr(rk, "comm", None) is not None:
             return r, rk.comm.allgather_batch(b, total)[0]
         return r, b.poses()
 
@@ -482,6 +517,13 @@ def bench_c4(args, rk, torch):
     pmc = "c4x1024_block" if (info["mode"] == "block" and n == wl["n"] and total == wl["problems"]
                               and rk.world == 1 and R == 50) else None
     roof = _resident_bound(_roofline(b, R, launch_us, pmc))
+    if solo:  # this GPU solved f1 - f0 of the batch's frames
+        out = {"frames": f1 - f0, "value": round((f1 - f0) * R * args.steps / elapsed, 2), "unit": "iterations/s",
+               "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "kernel_us": round(launch_us, 3),
+               "mode": b.info()["mode"], "blocks": b.info()["n_blocks"], "handoff_grid": b.residency()["handoff_grid"],
+               "timing": _sample_info(el_all, args.steps, (f1 - f0) * R, "iterations/s"), "pose_err_vs_gt_se3": err}
+        del b
+        return out
     out = {
         "metric": "PICP iterations/sec, batch of %d frames x %d correspondences" % (total, n),
         "value": round(total * R * args.steps / elapsed, 2),
@@ -503,9 +545,29 @@ def bench_c4(args, rk, torch):
                         "allgather_rows_match_local": bool(rk.max([0.0 if mine else 1.0])[0] == 0.0)}
     if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
         sz = int(bt["sizes"][0])
-        out["cpu_baseline"] = cpu_baseline(bt["xyz"][:sz], bt["uv"][:sz], bt["T_init"][0], R, args.cpu_seconds)
+        out["cpu_baseline"], T_or = cpu_baseline(bt["xyz"][:sz], bt["uv"][:sz], bt["T_init"][0], R, args.cpu_seconds)
+        out["pose_err_vs_oracle_se3_frame0"] = synth.se3_log_norm(b.poses()[0], T_or)
         out["cpu_baseline_all_cores"] = cpu_baseline_batch_mt(bt, R, args.cpu_seconds)
     return out
+
+
+def _c4_projection(args, rk, torch, v1):
+    """The per-rank shapes of the N = 2, 4, 8 C4 runs (the fixed 1024-frame batch split over N
+    GPUs: rank 0's 512, 256, 128 frames), each solved on this GPU alone.  projected_value = the
+    whole batch's rounds / the per-rank time (ranks are independent and equal-sized; the job's one
+    128-KB RCCL all-gather of the results is not included: it cannot be timed on one GPU, and it
+    is one collective per K-step job); efficiency = projected / (N x the 1-GPU value)."""
+    wl = WORKLOADS["c4"]
+    total = args.problems or wl["problems"]
+    per, proj = {}, {}
+    for N in (2, 4, 8):
+        r = bench_c4(args, rk, torch, shard=(N, 0))
+        per["n%d" % N] = r
+        pv = r["value"] * total / r["frames"]
+        proj["n%d" % N] = {"projected_value": round(pv, 1), "efficiency": round(pv / (N * v1), 4) if v1 else None}
+    proj["basis"] = ("per-rank time of rank 0's share measured on one GPU; excludes the all-gather of the results "
+                     "(one per job); the driver's multi-GPU run measures the real curve")
+    return per, proj
 
 
 def streaming_roofline(n, R, device):
@@ -535,26 +597,49 @@ def streaming_roofline(n, R, device):
             "pose_err_vs_gt_se3": err}
 
 
-def bench_vo(args, rk, torch):
-    """C5: the whole sequence is split into contiguous segments of --seg-len PICP steps (one-frame
-    overlap); ranks take contiguous ranges of segments (strong scaling: the
-    sequence is fixed).  One step = one run of this rank's segments (pair matching of all its
+_VO_CACHE = {}
+
+
+def _vo_frames(F, obs, fa, fb):
+    """The synthetic sequence (seed 42) and its packed frames fa .. fb (cached: the C5 lines share
+    one sequence)."""
+    from picp_amd.vo_synth import VOSequence
+    key = (F, obs)
+    if key not in _VO_CACHE:
+        _VO_CACHE.clear()
+        _VO_CACHE[key] = (VOSequence(F, obs_per_frame=obs, seed=42), {})
+    seq, frames = _VO_CACHE[key]
+    if (fa, fb) not in frames:
+        frames.clear()
+        frames[(fa, fb)] = seq.frames(fa, fb + 1)
+    return seq, frames[(fa, fb)]
+
+
+def bench_vo(args, rk, torch, seg_len=None, shard=None, tag="c5"):
+    """C5: the whole sequence is split into contiguous segments of seg_len (--seg-len) PICP steps
+    (one-frame overlap); ranks take contiguous ranges of segments (strong scaling:
+    the sequence is fixed).  One step = one run of this rank's segments (pair matching of all its
     frames, bootstrap, then per frame: world match, PICP block kernel with the gather fused in,
-    triangulate/append).
-    value = frames estimated by all ranks / max-over-ranks time."""
+    triangulate/append).  value = frames estimated by all ranks / max-over-ranks time.
+    shard=(world, rank): run that rank's share of the partition on this GPU alone (the per-rank
+    shape of an N-GPU run, measured on one GPU).
+    The line also carries the whole-sequence trajectory: the segments stitched at their one-frame
+    overlaps (picp_amd/evaluate.py) and its ATE after the reference's umeyama alignment
+    (src/my_utilities.cpp:459-478)."""
     import numpy as np
     import picp_amd
     from picp_amd import synth
-    from picp_amd.vo_synth import VOSequence, segments
+    from picp_amd.evaluate import ate, stitch_segments
+    from picp_amd.vo_synth import segments
     wl = WORKLOADS["c5"]
     F = args.frames or wl["frames"]
     obs = args.obs or wl["obs"]
-    L = args.seg_len
-    seq = VOSequence(F, obs_per_frame=obs, seed=42)
+    L = seg_len or args.seg_len
     first, steps = segments(F, L)
-    s0, s1 = picp_amd.shard_range(len(first), rk.world, rk.rank)
+    world, rank = shard if shard else (rk.world, rk.rank)
+    s0, s1 = picp_amd.shard_range(len(first), world, rank)
     fa, fb = int(first[s0]), int(first[s1 - 1] + steps[s1 - 1])
-    D = seq.frames(fa, fb + 1)
+    seq, D = _vo_frames(F, obs, fa, fb)
     my_first, my_steps = first[s0:s1] - fa, steps[s0:s1]
     # each segment's world frame is its first camera, as the reference's is frame 0's
     # (exec/icp_test.cpp:36, bootstrap from Identity): float32 coordinates stay segment-sized
@@ -592,9 +677,12 @@ def bench_vo(args, rk, torch):
     vo.set_segments(my_first, my_steps, boot, threshold=THRESHOLD)
     for _ in range(max(args.warmup, 1)):
         vo.run()
-    elapsed, ev_ms, el_all = _timed_samples(rk, torch, lambda: vo.time(args.steps), args.samples)
+    sync_ranks = shard is None  # a per-rank projection runs on this GPU alone
+    trk = rk if sync_ranks else _Solo()
+    elapsed, ev_ms, el_all = _timed_samples(trk, torch, lambda: vo.time(args.steps), args.samples)
     # correctness of what was timed: drift vs gt, PICP work done
-    P, Rr = vo.poses(), vo.step_records()
+    P, Rr, vinfo = vo.poses(), vo.step_records(), vo.info()
+    vo.close()
     err, rounds, corr = 0.0, 0, 0
     for k, f0 in enumerate(my_first):
         for t in range(1, len(P[k])):
@@ -604,15 +692,28 @@ def bench_vo(args, rk, torch):
             err = max(err, synth.se3_log_norm(est, gt))
         rounds += int(Rr[k]["rounds"][1:].sum())
         corr += int((Rr[k]["rounds"][1:].astype(np.int64) * Rr[k]["n_corr"][1:]).sum())
-    err = rk.max([err])[0]
-    tot = rk.gather_obj([rounds, corr, int(my_steps.sum())])
+    err = trk.max([err])[0]
+    tot = trk.gather_obj([rounds, corr, int(my_steps.sum())])
     rounds, corr, frames_total = (sum(t[i] for t in tot) for i in range(3))
-    info = vo.info()
+    # the whole trajectory: every rank's segments (gathered to all ranks, after timing), stitched
+    # at the one-frame overlaps from the ground-truth pose of frame first[s0] (segments in metric
+    # scale: gt-booted; essential-booted segments are scaled by their first baseline)
+    mine = [_scaled(P[k], scale[k]) for k in range(len(my_first))]
+    allP = trk.gather_obj((s0, mine))
+    allP.sort(key=lambda x: x[0])
+    segs = [p for _, ps in allP for p in ps]
+    g0 = allP[0][0]
+    gfirst, gsteps = first[g0:g0 + len(segs)], steps[g0:g0 + len(segs)]
+    frames, Tst = stitch_segments(segs, gfirst, gsteps, seq.T_cw(int(gfirst[0])))
+    traj = ate(Tst, np.stack([seq.T_cw(int(f)) for f in frames]))
+    traj["stitching"] = ("%d segments stitched at their one-frame overlaps, anchored at the ground truth of frame %d "
+                         "only; ATE after the similarity (umeyama, with scale) alignment of the positions, as "
+                         "the reference's alignTrajectories" % (len(segs), int(gfirst[0])))
     out = {
         "metric": "VO frames/sec (%d-frame synthetic sequence, ~%d obs/frame, per-frame match + PICP + triangulate)" % (F, obs),
         "value": round(frames_total * args.steps / elapsed, 2),
         "unit": "frames/s",
-        "n_gpus": rk.world,
+        "n_gpus": rk.world if sync_ranks else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
@@ -622,26 +723,56 @@ def bench_vo(args, rk, torch):
         "dtype": "f32",
         "data": "synthetic sequence (picp_amd/vo_synth.py, seed 42; observations resident in HBM)",
         "config": {"workload": wl["desc"], "frames": F, "obs_per_frame": obs, "segment_steps": L,
-                   "segments": len(first), "segments_this_rank": s1 - s0, "threshold": THRESHOLD,
+                   "segments": len(first), "segments_this_rank": s1 - s0,
+                   "partition": "%d %s %d-frame segments (%d PICP steps each), each bootstrapped from %s; %d on this "
+                                "GPU" % (len(first), "gt-anchored" if args.c5_boot == "gt" else "essential-bootstrapped",
+                                         L + 1, L, "its ground-truth pose pair" if args.c5_boot == "gt"
+                                         else "the two-view essential matrix", s1 - s0),
+                   "threshold": THRESHOLD,
                    "picp_loop": "icp_test: <= 50 rounds, relative chi convergence 1e-5",
-                   "parallelism": "contiguous segment ranges (picp_shard_range), one process per GPU"
-                   if rk.world > 1 else "single GPU",
-                   "block_npt": info["npt"]},
+                   "parallelism": ("contiguous segment ranges (picp_shard_range), one process per GPU"
+                                   if rk.world > 1 else "single GPU") if sync_ranks else
+                   "rank %d of %d's share, alone on one GPU (per-rank shape of the %d-GPU run)" % (rank, world, world),
+                   "block_npt": vinfo["npt"]},
         "timing": _sample_info(el_all, args.steps, frames_total, "frames/s"),
         "picp_iterations_per_s": round(rounds * args.steps / elapsed, 1),
         "picp_corr_rounds_per_s": round(corr * args.steps / elapsed, 1),
+        "chain_step_us": round(1e6 * elapsed / args.steps / max(1, int(my_steps.max())), 2),
         "timed_region_event_ms": round(ev_ms * args.steps, 4),
         "pose_err_vs_gt_se3_max": err,
         "pose_err_frame": "camera-in-world poses in each segment's frame (its first camera)",
+        "trajectory": traj,
         "bootstrap": boot_info,
     }
-    if rk.world > 1:
+    if rk.world > 1 and sync_ranks:
         out["ranks"] = {"world_size_observed": rk.comm.world,
                         "partition": [list(picp_amd.shard_range(len(first), rk.world, r)) for r in range(rk.world)]}
-    if rk.rank == 0 and rk.world == 1 and not args.no_cpu:
+    if rk.rank == 0 and rk.world == 1 and not args.no_cpu and tag == "c5":
         out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
         out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
     return out
+
+
+def _scaled(P, s):
+    """Poses with their translations scaled by s (a unit-baseline segment to metric)."""
+    import numpy as np
+    Q = np.array(P, np.float64)
+    Q[:, :3, 3] *= s
+    return Q
+
+
+class _Solo:
+    """Ranks-like stand-in for a measurement that runs on this process's GPU alone."""
+    world, rank = 1, 0
+
+    def barrier(self):
+        pass
+
+    def max(self, values):
+        return list(values)
+
+    def gather_obj(self, obj):
+        return [obj]
 
 
 def plan_only(args, rk):
@@ -841,14 +972,18 @@ def cpu_baseline(xyz, uv, T_init, R, budget_s):
     cols = _soa(xyz, uv)
     Kref = np.array(KREF, np.float32)
 
+    last = {}
+
     def one():
-        O.solve_soa(T_init, Kref, 480, 640, *cols, THRESHOLD, mode=O.MODE_FAITHFUL, max_rounds=R, conv_eps=-1.0)
+        last["T"], _ = O.solve_soa(T_init, Kref, 480, 640, *cols, THRESHOLD, mode=O.MODE_FAITHFUL, max_rounds=R,
+                                   conv_eps=-1.0)
         return R
 
     rate, rates, calls, el = _median_rate(one, budget_s)
-    return _cpu_result(rate, rates, "iterations/s", 1,
-                       "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, gcc -O3 "
-                       "-march=x86-64-v3, 1 thread) in %.1f s on %s" % (calls, R, len(cols[0]), el, _cpu_model()))
+    out = _cpu_result(rate, rates, "iterations/s", 1,
+                      "%d x %d-round solves of one %d-correspondence frame (faithful float32 oracle, gcc -O3 "
+                      "-march=x86-64-v3, 1 thread) in %.1f s on %s" % (calls, R, len(cols[0]), el, _cpu_model()))
+    return out, last["T"]
 
 
 if __name__ == "__main__":

@@ -336,6 +336,18 @@ def test_vo_segments_querying_one_frame(native, monkeypatch):
     seq = native.VOSequence(F["frame_off"], F["uv"], F["desc"], K=s.K)
     with pytest.raises(native.PicpError):
         seq.set_segments([0, 0], [5, 5], boot([0, 0]))
+    # equal first frames that are not adjacent collide too (segment 0 and 2 query frame 2 at
+    # step 0); a rejected call leaves the handle's previous segments in place
+    seq.set_segments([0, 3], [5, 5], boot([0, 3]), threshold=THR)
+    seq.run()
+    before = (seq.poses(), seq.step_records(), [seq.map(k) for k in range(2)])
+    with pytest.raises(native.PicpError):
+        seq.set_segments([1, 0, 1], [4, 4, 4], boot([1, 0, 1]))
+    with pytest.raises(native.PicpError):
+        seq.set_segments([0, 13], [5, 5], boot([0, 12]))  # out of range
+    seq.run()
+    _assert_same_bits(before, (seq.poses(), seq.step_records(), [seq.map(k) for k in range(2)]),
+                      "after rejected set_segments")
     seq.close()
     first, steps = np.array([0, 3]), np.array([8, 8])  # frames 4..9 queried by both, other steps
     monkeypatch.setenv("PICP_VO_OVERLAP", "0")
