@@ -28,7 +28,7 @@
 // hardware issues the older block first, so the two settle into alternating phases.
 #include <type_traits>
 
-#include "picp_device.h"
+#include "picp_vo_device.h"
 
 using namespace picp;
 
@@ -86,6 +86,9 @@ extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words
 // clamp did.  Needs n <= NPT*BS + lds_items and frames of <= VOG_CHUNKS*BS observations (the
 // host's check).  Writes a.probs[s] (the append reads n) and returns n.
 struct NoVo {};
+// VoT = VoAppend: the step's append (picp_vo_device.h vo_append_body) runs in the same block after
+// the rounds, on the final state in LDS, instead of in vo_append_kernel
+struct VoAppend : VoArgs {};
 #define VOG_CHUNKS 8  // observation chunks of BS held in registers: 4096 at BS 512
 #define VOG_SLICE 256  // items per pass of the register transfer
 template <int NPT, int BS>
@@ -232,7 +235,8 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
     unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks,
     const VoT vo, int vo_t) {
-  constexpr bool VOG = std::is_same<VoT, VoArgs>::value;  // the VO step's gather fused in
+  constexpr bool VOA = std::is_same<VoT, VoAppend>::value;  // ... and the append after the rounds
+  constexpr bool VOG = std::is_same<VoT, VoArgs>::value || VOA;  // the VO step's gather fused in
   PICP_KFENCE_IN();
   BSTAMP_PLACE();
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
@@ -489,6 +493,7 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
   if (split > 1 && tid == 0) tagbase[blockIdx.x] = tbase + (unsigned)last_round;
   if (h == 0 && tid < 32)
     reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
+  if constexpr (VOA) vo_append_body<BS>(vo, vo_t, vo.seg0 + p, &s_st, n);  // s_st: after the last barrier
   PICP_KFENCE_OUT();
 }
 
@@ -619,22 +624,29 @@ extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs) {
          (npt == 1 || npt == 2 || npt == 4 || npt == 8);
 }
 
+// append = 1: the step's append runs in the same kernel after the rounds (VoAppend); the caller
+// orders the launch after everything the append reads (the step's frame->next match).
 extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
-                                           const PicpArgs* args, int64_t max_obs) {
+                                           const PicpArgs* args, int64_t max_obs, int append) {
   if (!a || !args || a->n_seg <= 0 || !picp_vo_block_fusable(npt, max_obs)) return hipErrorInvalidValue;
   int lds_items = 0;
   const size_t lds_bytes = block_lds_bytes(npt, 1, (int)max_obs, &lds_items);
   const int var = picp_variant(args->K, args->keep_outliers);
-#define PICP_LAUNCH_VB3(N, P)                                                                               \
+  VoAppend va;
+  static_cast<VoArgs&>(va) = *a;
+#define PICP_LAUNCH_VB4(N, P, VT, VV)                                                                       \
   {                                                                                                        \
     if (lds_bytes > 65536)                                                                                 \
-      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>,                       \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, PICP_BBLOCK, VT>,                           \
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);                     \
-    hipLaunchKernelGGL((picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>), dim3(a->n_seg), dim3(PICP_BBLOCK),  \
+    hipLaunchKernelGGL((picp_block_kernel<N, P, PICP_BBLOCK, VT>), dim3(a->n_seg), dim3(PICP_BBLOCK),      \
                        lds_bytes, stream, a->X, a->Y, a->Z, a->U, a->V, *args, a->probs + a->seg0,          \
                        a->st_in + a->seg0, (PicpState*)a->st_out + a->seg0, lds_items, 1, a->n_seg,         \
-                       nullptr, nullptr, nullptr, 0ull, *a, t);                                            \
+                       nullptr, nullptr, nullptr, 0ull, VV, t);                                            \
   }
+#define PICP_LAUNCH_VB3(N, P)                 \
+  if (append) PICP_LAUNCH_VB4(N, P, VoAppend, va) \
+  else PICP_LAUNCH_VB4(N, P, VoArgs, *a)
 #define PICP_LAUNCH_VB(N)                                                        \
   if (var == PICP_V_PINHOLE) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE)                   \
   else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE_KEEP)    \
@@ -648,5 +660,6 @@ extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, 
   }
 #undef PICP_LAUNCH_VB
 #undef PICP_LAUNCH_VB3
+#undef PICP_LAUNCH_VB4
   return hipGetLastError();
 }

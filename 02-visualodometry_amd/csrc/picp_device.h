@@ -701,13 +701,13 @@ namespace picp {
 // Cross-lane moves without the LDS crossbar.  gfx950 v_permlane32_swap / v_permlane16_swap
 // exchange half-waves / odd-even 16-lane rows between two registers; DPP reads a partner
 // lane inside a 16-lane row (row_mirror l^15, row_half_mirror l^7, quad_perm l^2, l^1).
+// The lane's own value is the DPP "old" operand: with bound_ctrl off, a lane whose source lane is
+// disabled in EXEC keeps old instead of an undefined register (mov_dpp leaves it undefined).  Every
+// call site runs with EXEC full, so the results are the same either way; the defined form costs at
+// most a register copy per move.
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-#ifdef PICP_DPP_OLD
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
-#else
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-#endif
 }
 #define DPP_ROW_MIRROR 0x140
 #define DPP_ROW_HALF_MIRROR 0x141

@@ -45,6 +45,36 @@ __device__ inline void match_update(float d, int32_t j, float& best, float& seco
   bi = lt ? j : bi;
 }
 
+// One query's outputs: best index (relative to the problem's r_off), best and second distance,
+// and the reference's accept test (src/my_utilities.h:100-103: best < DISTANCE_THRESHOLD and
+// best/second < RATIO_THRESHOLD).  With P.merge the row already holds an earlier launch's top-2
+// over the references BEFORE this problem's (indices relative to that launch's r_off): the two
+// are merged as the reference's in-order scan would continue over this problem's references --
+// best = the smaller (a tie keeps the earlier, lower index), second = the second smallest of the
+// union (min of the larger best and the smaller side's second) -- and this launch's indices are
+// offset by P.idx_base.  Neither distance is ever NaN (match_update maps NaN to +inf).
+__device__ __forceinline__ void match_store(const MatchProblem& P, int64_t o, int32_t bi, float best, float second,
+                                            float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
+                                            float* second_dist, int32_t* accepted) {
+  if (P.merge) {
+    const float pb = best_dist[o], ps = second_dist[o];
+    const int32_t pi = best_idx[o];
+    const int32_t gi = (bi < 0) ? -1 : (int32_t)(bi + P.idx_base);
+    if (pb <= best) {
+      second = (ps < best) ? ps : best;
+      best = pb;
+      bi = pi;
+    } else {
+      second = (pb < second) ? pb : second;
+      bi = gi;
+    }
+  }
+  best_idx[o] = bi;
+  best_dist[o] = best;
+  second_dist[o] = second;
+  accepted[o] = (bi != -1 && best < dist_thr && best / second < ratio_thr) ? 1 : 0;
+}
+
 template <int D>  // D > 0: compile-time dim; D == 0: runtime dim <= PICP_MATCH_MAXD
 __global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
@@ -96,20 +126,12 @@ __global__ __launch_bounds__(PICP_MATCH_BLOCK) void picp_match_kernel(
     }
   }
   // accepted iff best < DISTANCE_THRESHOLD and best/second < RATIO_THRESHOLD (:100-103)
-  if (va) {
-    const int64_t o = P.q_off + qa;
-    best_idx[o] = bi_a;
-    best_dist[o] = best_a;
-    second_dist[o] = second_a;
-    accepted[o] = (bi_a != -1 && best_a < dist_thr && best_a / second_a < ratio_thr) ? 1 : 0;
-  }
-  if (vb) {
-    const int64_t o = P.q_off + qb;
-    best_idx[o] = bi_b;
-    best_dist[o] = best_b;
-    second_dist[o] = second_b;
-    accepted[o] = (bi_b != -1 && best_b < dist_thr && best_b / second_b < ratio_thr) ? 1 : 0;
-  }
+  if (va)
+    match_store(P, P.q_off + qa, bi_a, best_a, second_a, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                accepted);
+  if (vb)
+    match_store(P, P.q_off + qb, bi_b, best_b, second_b, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                accepted);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -817,11 +839,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
       }
     }
-    const int64_t o = P.q_off + qi;
-    best_idx[o] = bi;
-    best_dist[o] = best;
-    second_dist[o] = second;
-    accepted[o] = (bi != -1 && best < dist_thr && best / second < ratio_thr) ? 1 : 0;  // :100-103
+    match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                accepted);  // :100-103
   }
   PICP_KFENCE_OUT();
 }
