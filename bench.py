@@ -55,7 +55,13 @@ HANDOFF_US = 0.8       # MI355X_MICROARCH.md price list, handoff-1to1 (idle, 8-B
 FANIN_PAIR_US = 4.2    # price list, fanin: a 1->255 broadcast plus its 255->1 fan-in (idle, low end)
 FANIN_ARRIVAL_US = 0.012  # price list, fanin: ~11-13 ns per arrival
 FLOPS_PER_CORR = 160   # FP32 flops per correspondence-round (projection, J, J^T J, J^T e)
-VALU_PEAK_TFS = 157.3  # MI355X_MICROARCH.md chip table: peak FP32 vector
+VALU_PEAK_TFS = 157.3  # MI355X_MICROARCH.md chip table: peak FP32 vector (packed FP32: v_pk_fma_f32)
+# The device code is built without packed FP32 (hipcc_nopk.sh): its attainable FP32
+# vector ceiling is the unpacked rate, 256 CUs x 4 SIMDs x 16 FMA lanes x 2 flops x 2.4 GHz
+VALU_PEAK_SCALAR_TFS = 78.6
+SIMDS = 1024           # 256 CUs x 4
+VALU_ISSUE_CYCLES = 4  # one wave64 VALU instruction per 4 cycles per SIMD (16 lanes)
+CLOCK_GHZ = 2.4        # nominal shader clock (MI355X_MICROARCH.md; under load it can run lower)
 
 WORKLOADS = {
     "c2": dict(n=100000, problems=1, outlier=0.0, desc="C2 single-frame PICP, 100k synthetic correspondences, 50 GN rounds"),
@@ -247,11 +253,40 @@ def _roofline(b, R, launch_us, pmc_name):
            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
            "kernel": _kernel_name(info["mode"]), "mode": info["mode"], "kernel_us": round(launch_us, 3),
            "bytes_per_launch": per_launch, "blocks_per_launch": info["n_blocks"]}
-    # the FP32 vector view: 160 flops per correspondence-round over the same launch period
+    # the FP32 vector view: 160 flops per correspondence-round over the same launch period, against
+    # the unpacked ceiling this build can reach (and the packed spec beside it)
     tfs = FLOPS_PER_CORR * corr_per_launch / (launch_us * 1e-6) / 1e12 if launch_us > 0 else 0.0
-    out["valu"] = {"achieved": round(tfs, 3), "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
-                   "frac": round(tfs / VALU_PEAK_TFS, 5), "flops_per_launch": FLOPS_PER_CORR * corr_per_launch}
+    out["valu"] = {"achieved": round(tfs, 3), "peak": VALU_PEAK_SCALAR_TFS, "unit": "TFLOP/s",
+                   "frac": round(tfs / VALU_PEAK_SCALAR_TFS, 5), "peak_packed_fp32": VALU_PEAK_TFS,
+                   "frac_of_packed": round(tfs / VALU_PEAK_TFS, 5),
+                   "flops_per_launch": FLOPS_PER_CORR * corr_per_launch}
+    issue = pmc_issue(pmc_name, launch_us) if pmc_name else None
+    if issue:
+        out["valu"]["issue"] = issue
     return out
+
+
+def pmc_issue(name, launch_us):
+    """VALU issue-bound fraction of a launch from the newest committed SQ pass of the same command
+    (profiles/rNN/<name>_pmc_SQ.json: SQ_INSTS_VALU = wave-instructions per launch): the issue
+    capacity of one launch is 1024 SIMDs x one wave64 VALU instruction per 4 cycles at 2.4 GHz over
+    the launch time (the clock is nominal: under load it can be lower, so the fraction is a floor)."""
+    import glob
+    for d in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*")))):
+        f = os.path.join(d, "%s_pmc_SQ.json" % name)
+        if os.path.exists(f):
+            q = json.load(open(f))
+            valu = q["SQ_INSTS_VALU"]["mean"]
+            cap = SIMDS * launch_us * 1e-6 * CLOCK_GHZ * 1e9 / VALU_ISSUE_CYCLES
+            out = {"valu_wave_instr_per_launch": valu, "issue_capacity_per_launch": round(cap),
+                   "frac": round(valu / cap, 4), "source": os.path.relpath(f, ROOT),
+                   "basis": "SQ_INSTS_VALU / (1024 SIMDs x launch time x 2.4 GHz / 4 cycles per wave64 VALU)"}
+            if "SQ_WAVES" in q:
+                out["valu_per_wave"] = round(valu / max(q["SQ_WAVES"]["mean"], 1.0), 1)
+            if "GRBM_GUI_ACTIVE" in q:
+                out["grbm_gui_active"] = q["GRBM_GUI_ACTIVE"]["mean"]
+            return out
+    return None
 
 
 def _resident_bound(roof):
@@ -513,15 +548,18 @@ def bench_c4(args, rk, torch, shard=None):
     err = rk.max([err])[0]
     mine = np.array_equal(allT[f0:f1], b.poses())  # the gather put this rank's rows in place
     info = b.info()
-    # PMC passes of this exact command (1024 frames on one GPU): tools/gpu_pmc_r02.sh
-    pmc = "c4x1024_block" if (info["mode"] == "block" and n == wl["n"] and total == wl["problems"]
-                              and rk.world == 1 and R == 50) else None
+    # PMC passes of the same kernel shape (tools/r04/gpu_prof_r04.sh): 1024 frames on one GPU, or
+    # the 128-frame per-rank shape of an 8-GPU run
+    shape = {1024: "c4x1024_block", 128: "c4x128"}.get(f1 - f0)
+    pmc = shape if (info["mode"] == "block" and n == wl["n"] and R == 50 and (rk.world == 1 or solo)) else None
     roof = _resident_bound(_roofline(b, R, launch_us, pmc))
     if solo:  # this GPU solved f1 - f0 of the batch's frames
         out = {"frames": f1 - f0, "value": round((f1 - f0) * R * args.steps / elapsed, 2), "unit": "iterations/s",
                "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "kernel_us": round(launch_us, 3),
                "mode": b.info()["mode"], "blocks": b.info()["n_blocks"], "handoff_grid": b.residency()["handoff_grid"],
-               "timing": _sample_info(el_all, args.steps, (f1 - f0) * R, "iterations/s"), "pose_err_vs_gt_se3": err}
+               "timing": _sample_info(el_all, args.steps, (f1 - f0) * R, "iterations/s"), "pose_err_vs_gt_se3": err,
+               "roofline": {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                 "traffic_source", "issue") if k in roof}}
         del b
         return out
     out = {
