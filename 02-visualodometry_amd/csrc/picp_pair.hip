@@ -6,13 +6,15 @@
 // partner exchange of a split frame, the damped 6x6 solve and the pose update on one wave -- during
 // which the CU's other waves wait at a barrier: at the 128-frame per-rank shape of an 8-GPU C4 run
 // that tail is a third of the round.  Here a block holds part h of frame A and
-// part h of frame B (the same `split` blocks hold both frames), with 8 worker waves and one
-// finishing wave:
+// part h of frame B (the same `split` blocks hold both frames), with 8 worker waves and two
+// finishing waves, one per frame:
 //   * the workers linearize A (round r), publish their wave sums to LDS and go straight on to B
 //     (round r), then to A (round r + 1) as soon as its pose is there, ... -- no block barrier;
-//   * the finishing wave (issue priority 3: its chain of dependent instructions goes first when it
+//   * A's finishing wave (issue priority 3: its chain of dependent instructions goes first when it
 //     is ready) takes A's sums when all 8 workers have arrived, combines them, exchanges them with
-//     A's other parts, solves and publishes A's next pose to LDS -- while the workers linearize B.
+//     A's other parts, solves and publishes A's next pose to LDS -- while the workers linearize B;
+//     B's finishing wave does the same for B, overlapping A's (one finishing wave for both frames
+//     measured slower than split 4 alone: its two tails in series were longer than a linearize).
 // Hand-offs inside the block are LDS counters with workgroup-scope release/acquire: arrivals
 // (cumulative, 8 per round) and a per-frame generation (the rounds whose pose is in s_pose).
 //
@@ -32,7 +34,7 @@
 using namespace picp;
 
 #define PP_WORK 512              // worker threads: 8 waves, 2 per SIMD
-#define PP_BS (PP_WORK + 64)     // + the finishing wave
+#define PP_BS (PP_WORK + 128)    // + one finishing wave per frame
 #define PP_NW (PP_WORK / 64)
 #define PP_XG 64                 // exchange granules per (block, frame, round parity)
 #define PP_LDS_ITEMS 3840        // LDS stage per frame: 2 x 5 x 4 B x 3840 = 150 KB
@@ -228,113 +230,97 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
     return;
   }
 
-  // ---------------- the finishing wave
+  // ---------------- the finishing waves: wave 8 + f finishes frame f's rounds, so the two frames'
+  // tails (each a dependent chain: the combine, the partner exchange, the solve) overlap each other
+  // as well as the workers' linearize
   __builtin_amdgcn_s_setprio(3);
+  const int f = wave - PP_NW;
   pgu64_t* const xgg = (pgu64_t*)xg;
-  unsigned tbase[2] = {0u, 0u};
-  if (split > 1) {
-    tbase[0] = tagbase[2 * blockIdx.x];
-    tbase[1] = tagbase[2 * blockIdx.x + 1];
-  }
-  float pr[2][9], pt[2][3], chi_prev[2] = {FLT_MAX, FLT_MAX};
+  const unsigned tbase = (split > 1) ? tagbase[2 * blockIdx.x + f] : 0u;
+  float pr[9], pt[3], chi_prev = FLT_MAX;
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
+  for (int i = 0; i < 9; ++i) pr[i] = s_pose[f][i];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) pr[f][i] = s_pose[f][i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) pt[f][i] = s_pose[f][9 + i];
-  }
-  bool fin[2] = {s_done[0] != 0, s_done[1] != 0};
-  int rr[2] = {1, 1}, last_round[2] = {0, 0};
+  for (int i = 0; i < 3; ++i) pt[i] = s_pose[f][9 + i];
+  int last_round = 0;
   const unsigned g0 = ((blockIdx.x >> 3) / (unsigned)split) * (unsigned)split;  // part 0's group
-  while (!(fin[0] && fin[1])) {
+  bool done = s_done[f] != 0;
+  for (int round = 1; !done; ++round) {
+    bool tmo = !lds_wait_ge(&s_arr[f], PP_NW * round, timeout_ticks);
+    if (lane < PICP_NPART && !tmo) {  // fixed-order combine of the 8 waves, one lane per term
+      float ws[PP_NW];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      if (fin[f]) continue;
-      const int round = rr[f];
-      bool tmo = !lds_wait_ge(&s_arr[f], PP_NW * round, timeout_ticks);
-      if (lane < PICP_NPART && !tmo) {  // fixed-order combine of the 8 waves, one lane per term
-        float ws[PP_NW];
+      for (int w = 0; w < PP_NW; ++w) ws[w] = s_wave[f][lane][w];
+      double t = (double)ws[0];
 #pragma unroll
-        for (int w = 0; w < PP_NW; ++w) ws[w] = s_wave[f][lane][w];
-        double t = (double)ws[0];
+      for (int w = 1; w < PP_NW; ++w) t += (double)ws[w];
+      if (split > 1) {
+        // publish {round, hi}, {round, lo}; poll the partners'; add the parts in part order
+        const float hi = (float)t, lo = (float)(t - (double)hi);
+        const size_t slot = (size_t)(round & 1) * gridDim.x;
+        pgu64_t* mine = xgg + ((slot + blockIdx.x) * 2 + f) * PP_XG;
+        const unsigned tag = tbase + (unsigned)round;
+        __hip_atomic_store(mine + lane, ((unsigned long long)tag << 32) | __float_as_uint(hi), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(mine + PICP_NPART + lane, ((unsigned long long)tag << 32) | __float_as_uint(lo),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
+        double part_t[4];
+        unsigned pending = 0;
 #pragma unroll
-        for (int w = 1; w < PP_NW; ++w) t += (double)ws[w];
-        if (split > 1) {
-          // publish {round, hi}, {round, lo}; poll the partners'; add the parts in part order
-          const float hi = (float)t, lo = (float)(t - (double)hi);
-          const size_t slot = (size_t)(round & 1) * gridDim.x;
-          pgu64_t* mine = xgg + ((slot + blockIdx.x) * 2 + f) * PP_XG;
-          const unsigned tag = tbase[f] + (unsigned)round;
-          __hip_atomic_store(mine + lane, ((unsigned long long)tag << 32) | __float_as_uint(hi), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(mine + PICP_NPART + lane, ((unsigned long long)tag << 32) | __float_as_uint(lo),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
-          double part_t[4];
-          unsigned pending = 0;
+        for (int q = 0; q < 4; ++q) {
+          part_t[q] = 0.0;
+          if (q < split && q != h) pending |= 1u << q;
+        }
+        part_t[h & 3] = (double)hi + (double)lo;
+        for (;;) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            part_t[q] = 0.0;
-            if (q < split && q != h) pending |= 1u << q;
-          }
-          part_t[h & 3] = (double)hi + (double)lo;
-          for (;;) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (!(pending & (1u << q))) continue;
-              const pgu64_t* theirs = xgg + ((slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * 2 + f) * PP_XG;
-              const unsigned long long gh =
-                  __hip_atomic_load(theirs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              const unsigned long long gl =
-                  __hip_atomic_load(theirs + PICP_NPART + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) {
-                part_t[q] = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
-                pending &= ~(1u << q);
-              }
-            }
-            if (!pending) break;
-            if (__builtin_amdgcn_s_memrealtime() > deadline) {
-              tmo = true;
-              break;
+            if (!(pending & (1u << q))) continue;
+            const pgu64_t* theirs = xgg + ((slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * 2 + f) * PP_XG;
+            const unsigned long long gh = __hip_atomic_load(theirs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long gl =
+                __hip_atomic_load(theirs + PICP_NPART + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) {
+              part_t[q] = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
+              pending &= ~(1u << q);
             }
           }
-          t = part_t[0];
-#pragma unroll
-          for (int q = 1; q < 4; ++q)
-            if (q < split) t += part_t[q];
+          if (!pending) break;
+          if (__builtin_amdgcn_s_memrealtime() > deadline) {
+            tmo = true;
+            break;
+          }
         }
-        s_tot[f][lane] = total_word(A, lane, t);  // lane e converts total e
-      }
-      tmo = __any(tmo);  // wave-uniform
-      if (tmo) __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_wave_barrier();
-      RoundOut o;
-      finish_round_pose<PICP_FINISH_WAVE>(A, s_tot[f], round, pr[f], pt[f], chi_prev[f], o);
-      if (tmo) o.done = 1;  // stop (the host reports the error and re-runs the batch)
-      if (lane == 0) {
+        t = part_t[0];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) s_pose[f][i] = pr[f][i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) s_pose[f][9 + i] = pt[f][i];
-        s_done[f] = o.done;
-        if (o.done) store_state(&s_st[f], pr[f], pt[f], chi_prev[f], o, round);
-        __hip_atomic_store(&s_gen[f], round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int q = 1; q < 4; ++q)
+          if (q < split) t += part_t[q];
       }
-      last_round[f] = round;
-      fin[f] = o.done != 0;
-      ++rr[f];
+      s_tot[f][lane] = total_word(A, lane, t);  // lane e converts total e
     }
+    tmo = __any(tmo);  // wave-uniform
+    if (tmo) __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_wave_barrier();
+    RoundOut o;
+    finish_round_pose<PICP_FINISH_WAVE>(A, s_tot[f], round, pr, pt, chi_prev, o);
+    if (tmo) o.done = 1;  // stop (the host reports the error and re-runs the batch)
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) s_pose[f][i] = pr[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) s_pose[f][9 + i] = pt[i];
+      s_done[f] = o.done;
+      if (o.done) store_state(&s_st[f], pr, pt, chi_prev, o, round);
+      __hip_atomic_store(&s_gen[f], round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    last_round = round;
+    done = o.done != 0;  // every lane computed the same o
   }
   // every partner read its base before publishing round 1, and has finished its last round
-  if (split > 1 && lane < 2) tagbase[2 * blockIdx.x + lane] = tbase[lane] + (unsigned)last_round[lane];
-  __builtin_amdgcn_wave_barrier();
-  if (h == 0 && lane < 32) {
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-      if (2 * g + f < n_problems)
-        reinterpret_cast<int32_t*>(&st_out[2 * g + f])[lane] = reinterpret_cast<const int32_t*>(&s_st[f])[lane];
-  }
+  if (split > 1 && lane == 0) tagbase[2 * blockIdx.x + f] = tbase + (unsigned)last_round;
+  if (h == 0 && lane < 32 && 2 * g + f < n_problems)
+    reinterpret_cast<int32_t*>(&st_out[2 * g + f])[lane] = reinterpret_cast<const int32_t*>(&s_st[f])[lane];
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -292,12 +292,15 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
       HIP_TRY(hipEventCreateWithFlags(&h->ev_ph[c], hipEventDisableTiming));
     }
     if (h->split) {
+      // PICP_VO_EPRIO=0|1: the early parts' streams at the lowest / highest priority
+      const char* ee = getenv("PICP_VO_EPRIO");
+      const bool eprio_hi = !(ee && atoi(ee) == 0);
       h->estream.assign((size_t)h->chains, nullptr);
       h->ev_app.assign((size_t)h->chains, nullptr);
       h->ev_early.assign((size_t)2 * h->chains, nullptr);
       HIP_TRY(hipEventCreateWithFlags(&h->ev_boot, hipEventDisableTiming));
       for (int c = 0; c < h->chains; ++c) {
-        HIP_TRY(hipStreamCreateWithPriority(&h->estream[c], hipStreamNonBlocking, hi));
+        HIP_TRY(hipStreamCreateWithPriority(&h->estream[c], hipStreamNonBlocking, eprio_hi ? hi : lo));
         HIP_TRY(hipEventCreateWithFlags(&h->ev_app[c], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c + 1], hipEventDisableTiming));
