@@ -392,11 +392,14 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
       Acc a;
       acc_zero(a);
       accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
-      for (int i = tid; i < n_lds; i += BS)  // LDS-staged items
-        accumulate_item<PH>(T, C, thr, inv_thr, keep, lx[i], ly[i], lz[i], lu[i], lv[i], true, a, nd);
-      for (int i = r0 + n_lds + tid; i < n; i += BS)  // streamed remainder
-        accumulate_item<PH>(T, C, thr, inv_thr, keep, X[base + i], Y[base + i], Z[base + i], U[base + i],
-                            V[base + i], true, a, nd);
+      accumulate_stream1<PH>(T, C, thr, inv_thr, keep, tid, BS, n_lds,  // LDS-staged items
+                             [&](int i, float& x, float& y, float& z, float& u, float& v) {
+                               x = lx[i]; y = ly[i]; z = lz[i]; u = lu[i]; v = lv[i];
+                             }, a, nd);
+      accumulate_stream1<PH>(T, C, thr, inv_thr, keep, r0 + n_lds + tid, BS, n,  // streamed remainder
+                             [&](int i, float& x, float& y, float& z, float& u, float& v) {
+                               x = X[base + i]; y = Y[base + i]; z = Z[base + i]; u = U[base + i]; v = V[base + i];
+                             }, a, nd);
       BSTAMP(1);
       acc_fold(a, v);
     }

@@ -512,6 +512,107 @@ __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C,
   acc2_normal<true, KEEP>(J0, J1, e0, e1, w, a);
 }
 
+// A pair of correspondences, pinhole K, into ONE accumulation slot: accumulate_pinhole2's math on
+// float2 (two independent dependency chains through the projection, the gate and the Jacobian:
+// the instruction-level parallelism the two-slot form buys), then item A's terms and item B's
+// terms added into the same sums in that order -- exactly accumulate_pinhole(A) followed by
+// accumulate_pinhole(B), so the sums are the one-slot form's bits.  A skipped item's J and e are
+// zeroed (exact zeros: fma(+-0, x, h) == h, the sums never being -0), as accumulate_pinhole's
+// zeroing path does.
+template <bool KEEP, int RCP = RCP_CHECK>
+__device__ __forceinline__ void accumulate_pinhole_p1(const Pose& T, const Cam& C, float thr, float inv_thr,
+                                                      f2 x, f2 y, f2 z, f2 u, f2 v, bool inA, bool inB, Acc& a,
+                                                      Cnt& n) {
+  f2 pc0, pc1, pc2, ph0, ph1, iz, e0, e1, chi;
+  bool validA, validB;
+  {
+#pragma clang fp contract(off)
+    pc0 = ((T.r00 * x + T.r01 * y) + T.r02 * z) + T.t0;  // src/camera.h:26
+    pc1 = ((T.r10 * x + T.r11 * y) + T.r12 * z) + T.t1;
+    pc2 = pair_depth(T, x, y, z);
+    ph0 = C.k00 * pc0 + C.k02 * pc2;  // src/camera.h:29 without the zero terms
+    ph1 = C.k11 * pc1 + C.k12 * pc2;
+    if (RCP == RCP_FAST || (RCP == RCP_CHECK && __all(rcp_safe(pc2.x) & rcp_safe(pc2.y)))) {
+      iz.x = rcp_rn(pc2.x);
+      iz.y = rcp_rn(pc2.y);
+    } else {
+      iz.x = 1.0f / pc2.x;
+      iz.y = 1.0f / pc2.y;
+    }
+    const f2 ix = ph0 * iz;
+    const f2 iy = ph1 * iz;
+    validA = inA & !(pc2.x <= 0.0f) & !((ix.x < 0.0f) | (ix.x > C.maxx) | (iy.x < 0.0f) | (iy.x > C.maxy));
+    validB = inB & !(pc2.y <= 0.0f) & !((ix.y < 0.0f) | (ix.y > C.maxx) | (iy.y < 0.0f) | (iy.y > C.maxy));
+    e0 = ix - u;
+    e1 = iy - v;
+    chi = e0 * e0 + e1 * e1;
+  }
+  const bool outA = chi.x > thr, outB = chi.y > thr;
+  const bool inlA = validA & !outA, inlB = validB & !outB;
+  const bool useA = inlA | (validA & KEEP), useB = inlB | (validB & KEEP);
+  f2 w = {1.0f, 1.0f};
+  if constexpr (KEEP) {
+    const f2 q = chi * inv_thr;
+    w = (f2){useA ? (inlA ? 1.0f : __builtin_amdgcn_rsqf(q.x)) : 0.0f,
+             useB ? (inlB ? 1.0f : __builtin_amdgcn_rsqf(q.y)) : 0.0f};
+  }
+  a.chi_in += inlA ? chi.x : 0.0f;  // item A, then item B: the one-slot order
+  a.chi_out += (validA & outA) ? chi.x : 0.0f;
+  a.chi_in += inlB ? chi.y : 0.0f;
+  a.chi_out += (validB & outB) ? chi.y : 0.0f;
+  cnt_add(n, inlA, validA);
+  cnt_add(n, inlB, validB);
+#define PICP_Z2(val) val = (f2){useA ? val.x : 0.0f, useB ? val.y : 0.0f}
+  PICP_Z2(iz); PICP_Z2(pc0); PICP_Z2(pc1); PICP_Z2(pc2); PICP_Z2(ph0); PICP_Z2(ph1); PICP_Z2(e0); PICP_Z2(e1);
+#undef PICP_Z2
+  f2 J0[6], J1[6];
+  {
+#pragma clang fp contract(off)
+    const f2 iz2 = iz * iz;  // src/picp_solver.cpp:45-52, the oracle's operation order
+    const f2 jp0 = -(ph0 * iz2), jp1 = -(ph1 * iz2);
+    const f2 a00 = iz * C.k00, a02 = iz * C.k02 + jp0;
+    const f2 a11 = iz * C.k11, a12 = iz * C.k12 + jp1;
+    const f2 zero = {0.0f, 0.0f};
+    J0[0] = a00; J0[1] = zero; J0[2] = a02;
+    J0[3] = a02 * pc1;
+    J0[4] = a00 * pc2 - a02 * pc0;
+    J0[5] = -(a00 * pc1);
+    J1[0] = zero; J1[1] = a11; J1[2] = a12;
+    J1[3] = -(a11 * pc2) + a12 * pc1;
+    J1[4] = -(a12 * pc0);
+    J1[5] = a11 * pc0;
+  }
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {  // item A's terms, then item B's (accumulate_pinhole's order)
+    float W0[6], W1[6], K0[6], K1[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      K0[i] = it ? J0[i].y : J0[i].x;
+      K1[i] = it ? J1[i].y : J1[i].x;
+      const float wi = it ? w.y : w.x;
+      W0[i] = KEEP ? wi * K0[i] : K0[i];
+      W1[i] = KEEP ? wi * K1[i] : K1[i];
+    }
+    const float f0 = it ? e0.y : e0.x, f1 = it ? e1.y : e1.x;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+      for (int j = i; j < 6; ++j) {
+        float h = a.h[k];
+        if (i != 0 && j != 0) h = fmaf(W1[i], K1[j], h);  // J1[0] == 0
+        if (i != 1 && j != 1) h = fmaf(W0[i], K0[j], h);  // J0[1] == 0
+        a.h[k] = h;
+        ++k;
+      }
+      float bb = a.b[i];
+      if (i != 0) bb = fmaf(W1[i], f1, bb);
+      if (i != 1) bb = fmaf(W0[i], f0, bb);
+      a.b[i] = bb;
+    }
+  }
+}
+
 // A pair of correspondences, general K: per-item math (item_general), paired accumulation.
 __device__ __forceinline__ void accumulate_general2(const Pose& T, const Cam& C, float thr, bool keep,
                                                     f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
@@ -580,6 +681,12 @@ __device__ __forceinline__ void accumulate_regs(const Pose& T, const Cam& C, flo
 // +2.7 %), the two-slot pair form at NPT 8 (C3 +5-9 %, C4 +17 %: its two independent
 // accumulation chains and its paired LDS/stream loops).  -DPICP_ACC_PAIRS / -DPICP_ACC_ONE force
 // one form for A/B builds.
+// One-slot accumulation with the per-item math in pairs (accumulate_pinhole_p1): the same bits
+// as item by item.  -DPICP_P1=0 restores the item-by-item form for A/B builds.
+#ifndef PICP_P1
+#define PICP_P1 1
+#endif
+
 __host__ __device__ constexpr bool acc_pairs(int npt) {
 #if defined(PICP_ACC_PAIRS)
   return true;
@@ -610,6 +717,25 @@ __device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, fl
 #pragma unroll
     for (int k = 0; k < NPT; ++k) fast &= rcp_safe(item_depth(T, xs[k], ys[k], zs[k]));
     auto run = [&](auto rcp) {
+      constexpr bool KP = PH == PICP_V_PINHOLE_KEEP;
+      constexpr int R = decltype(rcp)::value;
+#if PICP_P1
+      // items in pairs (k, k + 1) through accumulate_pinhole_p1: the same sums in the same order
+      // as item by item, with two dependency chains through the per-item math
+#pragma unroll
+      for (int k = 0; k + 1 < NPT; k += 2) {
+        const bool inA = first + k * stride < n, inB = first + (k + 1) * stride < n;
+        if (k + 2 < NPT || __any(inB))  // the last slot only in waves that hold an item there
+          accumulate_pinhole_p1<KP, R>(T, C, thr, inv_thr, (f2){xs[k], xs[k + 1]}, (f2){ys[k], ys[k + 1]},
+                                       (f2){zs[k], zs[k + 1]}, (f2){us[k], us[k + 1]}, (f2){vs[k], vs[k + 1]}, inA,
+                                       inB, a, cnt);
+        else
+          accumulate_pinhole<KP, R>(T, C, thr, inv_thr, xs[k], ys[k], zs[k], us[k], vs[k], inA, a, cnt);
+      }
+      if constexpr (NPT & 1)
+        accumulate_pinhole<KP, R>(T, C, thr, inv_thr, xs[NPT - 1], ys[NPT - 1], zs[NPT - 1], us[NPT - 1],
+                                  vs[NPT - 1], first + (NPT - 1) * stride < n, a, cnt);
+#else
 #pragma unroll
       for (int k = 0; k < NPT; ++k)
         // the last slot only in waves that hold an item there (a wave-uniform branch): a frame
@@ -617,8 +743,9 @@ __device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, fl
         // SIMDs in turn every SIMD then issues one slot less when n <= (NPT - 1/2) x BS (C5's
         // ~1,750 correspondences on 2,048 slots).  A skipped item adds exact zeros: same bits.
         if (NPT < 2 || k + 1 < NPT || __any(first + k * stride < n))
-          accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, decltype(rcp)::value>(T, C, thr, inv_thr, xs[k], ys[k], zs[k],
-                                                                             us[k], vs[k], first + k * stride < n, a, cnt);
+          accumulate_pinhole<KP, R>(T, C, thr, inv_thr, xs[k], ys[k], zs[k], us[k], vs[k], first + k * stride < n, a,
+                                    cnt);
+#endif
     };
     if (__all(fast))
       run(std::integral_constant<int, RCP_FAST>());
@@ -640,6 +767,37 @@ __device__ __forceinline__ void accumulate_item(const Pose& T, const Cam& C, flo
       accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_FAST>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
     else
       accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_DIV>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
+  }
+}
+
+// Streamed (LDS or HBM) items i, i + stride, i + 2 stride, ... (i = first) of one lane into one
+// slot, in that order: pairs through accumulate_pinhole_p1 (the fast reciprocal by a vote of the
+// lanes that run the pair), the general variant item by item.  get(i, x, y, z, u, v) loads item i.
+template <int PH, typename Get>
+__device__ __forceinline__ void accumulate_stream1(const Pose& T, const Cam& C, float thr, float inv_thr, bool keep,
+                                                   int first, int stride, int count, Get get, Acc& a, Cnt& n) {
+#if PICP_P1
+  if constexpr (PH != PICP_V_GENERAL) {
+    constexpr bool KP = PH == PICP_V_PINHOLE_KEEP;
+    for (int i = first; i < count; i += 2 * stride) {
+      const bool inB = i + stride < count;
+      const int j = inB ? i + stride : i;
+      float x0, y0, z0, u0, v0, x1, y1, z1, u1, v1;
+      get(i, x0, y0, z0, u0, v0);
+      get(j, x1, y1, z1, u1, v1);
+      const f2 x = {x0, x1}, y = {y0, y1}, z = {z0, z1};
+      if (__all(pair_rcp_safe(T, x, y, z)))
+        accumulate_pinhole_p1<KP, RCP_FAST>(T, C, thr, inv_thr, x, y, z, (f2){u0, u1}, (f2){v0, v1}, true, inB, a, n);
+      else
+        accumulate_pinhole_p1<KP, RCP_DIV>(T, C, thr, inv_thr, x, y, z, (f2){u0, u1}, (f2){v0, v1}, true, inB, a, n);
+    }
+    return;
+  }
+#endif
+  for (int i = first; i < count; i += stride) {
+    float x, y, z, u, v;
+    get(i, x, y, z, u, v);
+    accumulate_item<PH>(T, C, thr, inv_thr, keep, x, y, z, u, v, true, a, n);
   }
 }
 

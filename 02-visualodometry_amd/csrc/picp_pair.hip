@@ -41,6 +41,26 @@ using namespace picp;
 
 typedef __attribute__((address_space(1))) unsigned long long pgu64_t;
 
+// Diagnostic build only (-DPICP_STAMPS, tools/pair_stamps.py): s_memrealtime of rounds 11 and 12
+// of blocks < 256, per frame f: [0] worker wave 0 has the pose, [1] it has published its sums,
+// [2] the finishing wave has every arrival, [3] its partner exchange is done, [4] the new pose is
+// published.
+#ifdef PICP_STAMPS
+__device__ unsigned long long picp_pair_stamps[2][256][2][8];
+#define PSTAMPF(round, f, k)                                                                       \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && ((round) == 11 || (round) == 12) && blockIdx.x < 256)           \
+      picp_pair_stamps[(round) - 11][blockIdx.x][f][k] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+extern "C" hipError_t picp_debug_pair_stamps(unsigned long long* out, size_t n_words) {
+  const size_t cap = sizeof(picp_pair_stamps) / sizeof(unsigned long long);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_pair_stamps), (n_words < cap ? n_words : cap) * 8, 0,
+                             hipMemcpyDeviceToHost);
+}
+#else
+#define PSTAMPF(round, f, k) ((void)0)
+#endif
+
 __device__ __forceinline__ int lds_acquire(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -173,6 +193,7 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
           fin[f] = true;
           continue;
         }
+        if (wave == 0) PSTAMPF(rr[f], f, 0);
         Pose T;
         T.r00 = s_pose[f][0]; T.r10 = s_pose[f][1]; T.r20 = s_pose[f][2];
         T.r01 = s_pose[f][3]; T.r11 = s_pose[f][4]; T.r21 = s_pose[f][5];
@@ -209,14 +230,16 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
           acc_zero(a);
           accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs[f], ys[f], zs[f], us[f], vs[f], tid, PP_WORK, n[f],
                                     a, nr);
-          for (int i = tid; i < n_lds[f]; i += PP_WORK)  // LDS-staged items
-            accumulate_item<PH>(T, C, thr, inv_thr, keep, l[i], l[lds_items + i], l[2 * lds_items + i],
-                                l[3 * lds_items + i], l[4 * lds_items + i], true, a, nd);
-          for (int i = r0 + n_lds[f] + tid; i < n[f]; i += PP_WORK) {  // streamed remainder
-            const int64_t b = base[f];
-            accumulate_item<PH>(T, C, thr, inv_thr, keep, X[b + i], Y[b + i], Z[b + i], U[b + i], V[b + i], true, a,
-                                nd);
-          }
+          accumulate_stream1<PH>(T, C, thr, inv_thr, keep, tid, PP_WORK, n_lds[f],  // LDS-staged items
+                                 [&](int i, float& x, float& y, float& z, float& u, float& v) {
+                                   x = l[i]; y = l[lds_items + i]; z = l[2 * lds_items + i];
+                                   u = l[3 * lds_items + i]; v = l[4 * lds_items + i];
+                                 }, a, nd);
+          const int64_t b = base[f];
+          accumulate_stream1<PH>(T, C, thr, inv_thr, keep, r0 + n_lds[f] + tid, PP_WORK, n[f],  // streamed remainder
+                                 [&](int i, float& x, float& y, float& z, float& u, float& v) {
+                                   x = X[b + i]; y = Y[b + i]; z = Z[b + i]; u = U[b + i]; v = V[b + i];
+                                 }, a, nd);
           acc_fold(a, v);
         }
         const float wred = wave_reduce32(v, lane);
@@ -224,6 +247,7 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
         if ((lane & 1) == 0) s_wave[f][lane >> 1][wave] = wsum;
         // arrival: the release orders this wave's s_wave stores before the count
         if (lane == 0) __hip_atomic_fetch_add(&s_arr[f], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wave == 0) PSTAMPF(rr[f], f, 1);
         ++rr[f];
       }
     }
@@ -247,6 +271,7 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
   bool done = s_done[f] != 0;
   for (int round = 1; !done; ++round) {
     bool tmo = !lds_wait_ge(&s_arr[f], PP_NW * round, timeout_ticks);
+    PSTAMPF(round, f, 2);
     if (lane < PICP_NPART && !tmo) {  // fixed-order combine of the 8 waves, one lane per term
       float ws[PP_NW];
 #pragma unroll
@@ -299,6 +324,7 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
       }
       s_tot[f][lane] = total_word(A, lane, t);  // lane e converts total e
     }
+    PSTAMPF(round, f, 3);
     tmo = __any(tmo);  // wave-uniform
     if (tmo) __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_wave_barrier();
@@ -314,6 +340,7 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
       if (o.done) store_state(&s_st[f], pr, pt, chi_prev, o, round);
       __hip_atomic_store(&s_gen[f], round, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    PSTAMPF(round, f, 4);
     last_round = round;
     done = o.done != 0;  // every lane computed the same o
   }

@@ -124,7 +124,7 @@ struct picp_vo {
   // the chain's early stream beside step t-1, and the LATE part against the points step t-1's
   // append added (about one frame's new landmarks), on the chain, merged into the early part's
   // rows (picp_match.hip match_store).  The merged top-2 is the full match's, bit for bit.
-  int split = 1;
+  int split = 0;
   std::vector<hipStream_t> estream;  // [chains]: early parts
   std::vector<hipEvent_t> ev_app;    // [chains]: the chain's latest append (an early part may start)
   std::vector<hipEvent_t> ev_early;  // [chains][2]: early part of step t done (by step parity)
