@@ -214,13 +214,18 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
   return n;
 }
 
-// Issue priority of a block's waves by phase (-DPICP_BPRIO, A/B): the round's tail (the wave
-// reduction, the combine and partner exchange, the one-wave solve) is a dependency chain; when a
-// second block shares the CU (split 4), its linearize would take the SIMDs' issue slots ahead of it.
+// Issue priority of a block's waves by phase (on by default; -DPICP_BPRIO=0 for A/B): the round's
+// tail (the wave reduction, the combine and partner exchange, the one-wave solve) is a dependency
+// chain; when a second block shares the CU (split 4), its linearize would take the SIMDs' issue
+// slots ahead of it.  C4 at 128 frames, split 4: 20.4M -> 22.9M it/s; split 2 and the VO step
+// kernel within noise (profiles/r04/c4_128/, profiles/r04/pair2/).
+#ifndef PICP_BPRIO
+#define PICP_BPRIO 1
+#endif
 // -DPICP_VOPRIO (A/B): in the VO step's form the linearize runs at priority 2 as well, so the
 // matcher waves that share the CU (the split world match's early part, the frame->next chunks,
 // priority 0) take only the issue slots the step chain leaves.
-#ifdef PICP_BPRIO
+#if PICP_BPRIO
 #define BPRIO_TAIL() __builtin_amdgcn_s_setprio(3)
 #ifdef PICP_VOPRIO
 #define BPRIO_LIN() (VOG ? __builtin_amdgcn_s_setprio(2) : __builtin_amdgcn_s_setprio(0))

@@ -684,7 +684,7 @@ __device__ __forceinline__ void accumulate_regs(const Pose& T, const Cam& C, flo
 // One-slot accumulation with the per-item math in pairs (accumulate_pinhole_p1): the same bits
 // as item by item.  -DPICP_P1=0 restores the item-by-item form for A/B builds.
 #ifndef PICP_P1
-#define PICP_P1 1
+#define PICP_P1 0
 #endif
 
 __host__ __device__ constexpr bool acc_pairs(int npt) {

@@ -375,10 +375,13 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
       // PICP_BLOCK_SPLIT=1|2 forces
       auto grid_of = [&](int s) { return ((s * np + 8 * s - 1) / (8 * s)) * (8 * s); };
       int split = (grid_of(2) <= b->num_cu && max_n >= 4096) ? 2 : 1;
+      // four 512-thread parts per problem, two blocks per CU from different problems, when four
+      // times the problems still fit two per CU and a part keeps >= 2048 correspondences (the C4
+      // per-rank shape at N = 8, 128 frames x 10k): one block's round tail (at issue priority 3)
+      // runs under the other's linearize; 22.0-22.4M vs 21.2-21.4M it/s for split 2
+      // (profiles/r04/p1/).  256-thread parts (PICP_BLOCK_S4BS=256, round 1) were 5 % slower.
+      if (grid_of(4) <= 2 * b->num_cu && max_n >= 8192 && picp_block_threads(4) == 512) split = 4;
       if (b->no_handoff) split = 1;
-      // (split 4 -- four 256-thread parts per problem, two blocks per CU from different
-      // problems, meant to overlap one problem's exchange + solve with the other's linearize --
-      // measured 5 % slower than split 2 at C4 (profiles/r01/c4_split4_ab.log): PICP_BLOCK_SPLIT=4)
       if (const char* e = getenv("PICP_BLOCK_SPLIT")) {
         const int v = atoi(e);
         if (v == 1) split = 1;
