@@ -525,8 +525,8 @@ def bench_c4(args, rk, torch, shard=None):
     total = args.problems or wl["problems"]
     R = args.rounds
     solo = shard is not None
-    if solo:
-        rk = _Solo()
+    if solo:  # this GPU alone: no barriers, max or gather over the ranks
+        rk = _Solo(rk.device)
     f0, f1 = picp_amd.shard_range(total, *(shard if solo else (rk.world, rk.rank)))
     bt = synth.make_batch(f1 - f0, n, base_seed=1000, first=f0, outlier_frac=0.0, pixel_noise=0.5)
     b = picp_amd.Batch(bt["sizes"], device=rk.device)
@@ -716,7 +716,7 @@ def bench_vo(args, rk, torch, seg_len=None, shard=None, tag="c5"):
     for _ in range(max(args.warmup, 1)):
         vo.run()
     sync_ranks = shard is None  # a per-rank projection runs on this GPU alone
-    trk = rk if sync_ranks else _Solo()
+    trk = rk if sync_ranks else _Solo(rk.device)
     elapsed, ev_ms, el_all = _timed_samples(trk, torch, lambda: vo.time(args.steps), args.samples)
     # correctness of what was timed: drift vs gt, PICP work done
     P, Rr, vinfo = vo.poses(), vo.step_records(), vo.info()
@@ -801,7 +801,10 @@ def _scaled(P, s):
 
 class _Solo:
     """Ranks-like stand-in for a measurement that runs on this process's GPU alone."""
-    world, rank = 1, 0
+    world, rank, comm = 1, 0, None
+
+    def __init__(self, device=0):
+        self.device = device
 
     def barrier(self):
         pass
