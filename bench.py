@@ -277,14 +277,20 @@ def pmc_issue(name, launch_us):
         if os.path.exists(f):
             q = json.load(open(f))
             valu = q["SQ_INSTS_VALU"]["mean"]
-            cap = SIMDS * launch_us * 1e-6 * CLOCK_GHZ * 1e9 / VALU_ISSUE_CYCLES
+            if "GRBM_GUI_ACTIVE" in q:
+                # the profiled launch's own busy cycles (GRBM_GUI_ACTIVE summed over the 8 XCDs):
+                # capacity = 1024 SIMDs x those cycles / 4, independent of the clock it ran at
+                cyc = q["GRBM_GUI_ACTIVE"]["mean"] / 8.0
+                cap = SIMDS * cyc / VALU_ISSUE_CYCLES
+                basis = ("SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8 cycles / 4 cycles per wave64 VALU), both "
+                         "from the same profiled launches")
+            else:
+                cap = SIMDS * launch_us * 1e-6 * CLOCK_GHZ * 1e9 / VALU_ISSUE_CYCLES
+                basis = "SQ_INSTS_VALU / (1024 SIMDs x launch time x 2.4 GHz / 4 cycles per wave64 VALU)"
             out = {"valu_wave_instr_per_launch": valu, "issue_capacity_per_launch": round(cap),
-                   "frac": round(valu / cap, 4), "source": os.path.relpath(f, ROOT),
-                   "basis": "SQ_INSTS_VALU / (1024 SIMDs x launch time x 2.4 GHz / 4 cycles per wave64 VALU)"}
+                   "frac": round(valu / cap, 4), "source": os.path.relpath(f, ROOT), "basis": basis}
             if "SQ_WAVES" in q:
                 out["valu_per_wave"] = round(valu / max(q["SQ_WAVES"]["mean"], 1.0), 1)
-            if "GRBM_GUI_ACTIVE" in q:
-                out["grbm_gui_active"] = q["GRBM_GUI_ACTIVE"]["mean"]
             return out
     return None
 
