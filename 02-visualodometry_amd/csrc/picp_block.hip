@@ -256,7 +256,6 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
   __shared__ __attribute__((aligned(16))) float s_wave[PICP_NPART][BS / 64];
   __shared__ float s_tot[PICP_NPART];  // the totals as finish_round_f words (total_word)
   __shared__ float s_pose[12];
-  __shared__ int s_lite;  // s_pose within accumulate_pinhole2's LITE bounds (set with s_pose)
   __shared__ int s_done;
   __shared__ int s_tmo;  // a partner wait timed out (the error word is for the host)
   __shared__ PicpState s_st;
@@ -341,7 +340,6 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     for (int i = 0; i < 9; ++i) s_pose[i] = s.R[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
-    s_lite = (acc_pairs(NPT) || PICP_LITE1) && pose_lite(s.R, s.t);
     s_done = s.done;
     s_tmo = 0;
     s_st = s;
@@ -357,15 +355,6 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
   const float thr = A.threshold;
   const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
-  // the wave's register and LDS items all within accumulate_pinhole2's LITE bounds (checked once)
-  bool items_ok = acc_pairs(NPT) || PICP_LITE1;
-  if (items_ok) {
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) items_ok &= coords_lite(xs[k], ys[k], zs[k]);
-    for (int i = tid; i < n_lds; i += BS) items_ok &= coords_lite(lx[i], ly[i], lz[i]);
-  }
-  // per wave: a lane's LDS items (i = tid + k * BS) are exactly those the same lane checked
-  const bool items_lite = __all(items_ok) && cam_lite(C);
 
   // the icp_test loop state a round reads: the pose (s_pose, every wave) and chi_prev (wave 0,
   // which finishes the rounds, keeps it in a register)
@@ -381,28 +370,20 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     // accumulation form by register-resident items per lane (picp_device.h acc_pairs): two slots
     // for NPT 8, one slot below
     float v[PICP_NPART];
-    Cnt nr = {0u, 0u}, nd = {0u, 0u};  // counts: register items, LDS/streamed items (cnt_add)
+    Cnt nr = {0u, 0u}, nd = {0u, 0u};  // counts: register items (uniform), divergent loops (lane 0)
     if constexpr (acc_pairs(NPT)) {
       Acc2 a;
       acc2_zero(a);
-      const bool lite = wave_uniform(items_lite && s_lite != 0);
-      accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr, lite);
-      auto lds_pairs = [&](auto lt) {
-        for (int i = tid; i < n_lds; i += 2 * BS) {  // LDS-staged items, in pairs
-          const int i2 = min(i + BS, n_lds - 1);
-          // scalar locals first: building the f2 operands from the LDS reads directly made the
-          // compiler round-trip them through scratch every round
-          const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
-          const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
-          accumulate2<PH, RCP_CHECK, decltype(lt)::value>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1},
-                                                          (f2){z0, z1}, (f2){u0, u1}, (f2){v0, v1}, true,
-                                                          i + BS < n_lds, a, nd);
-        }
-      };
-      if (lite)
-        lds_pairs(std::true_type());
-      else
-        lds_pairs(std::false_type());
+      accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
+      for (int i = tid; i < n_lds; i += 2 * BS) {  // LDS-staged items, in pairs
+        const int i2 = min(i + BS, n_lds - 1);
+        // scalar locals first: building the f2 operands from the LDS reads directly made the
+        // compiler round-trip them through scratch every round
+        const float x0 = lx[i], y0 = ly[i], z0 = lz[i], u0 = lu[i], v0 = lv[i];
+        const float x1 = lx[i2], y1 = ly[i2], z1 = lz[i2], u1 = lu[i2], v1 = lv[i2];
+        accumulate2<PH>(T, C, thr, inv_thr, keep, (f2){x0, x1}, (f2){y0, y1}, (f2){z0, z1}, (f2){u0, u1},
+                        (f2){v0, v1}, true, i + BS < n_lds, a, nd);
+      }
       for (int i = r0 + n_lds + tid; i < n; i += 2 * BS) {  // streamed remainder
         const int i2 = min(i + BS, n - 1);
         const float x0 = X[base + i], y0 = Y[base + i], z0 = Z[base + i], u0 = U[base + i], v0 = V[base + i];
@@ -415,18 +396,11 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     } else {
       Acc a;
       acc_zero(a);
-      const bool lite = PICP_LITE1 && wave_uniform(items_lite && s_lite != 0);
-      accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr, lite);
-      auto lds_items = [&](auto lt) {
-        accumulate_stream1<PH, decltype(lt)::value>(T, C, thr, inv_thr, keep, tid, BS, n_lds,  // LDS-staged items
-                                                     [&](int i, float& x, float& y, float& z, float& u, float& v) {
-                                                       x = lx[i]; y = ly[i]; z = lz[i]; u = lu[i]; v = lv[i];
-                                                     }, a, nd);
-      };
-      if (lite)
-        lds_items(std::true_type());
-      else
-        lds_items(std::false_type());
+      accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, n, a, nr);
+      accumulate_stream1<PH>(T, C, thr, inv_thr, keep, tid, BS, n_lds,  // LDS-staged items
+                             [&](int i, float& x, float& y, float& z, float& u, float& v) {
+                               x = lx[i]; y = ly[i]; z = lz[i]; u = lu[i]; v = lv[i];
+                             }, a, nd);
       accumulate_stream1<PH>(T, C, thr, inv_thr, keep, r0 + n_lds + tid, BS, n,  // streamed remainder
                              [&](int i, float& x, float& y, float& z, float& u, float& v) {
                                x = X[base + i]; y = Y[base + i]; z = Z[base + i]; u = U[base + i]; v = V[base + i];
@@ -521,7 +495,6 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
         for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];
 #pragma unroll
         for (int i = 0; i < 3; ++i) s_pose[9 + i] = pt[i];
-        if constexpr (acc_pairs(NPT) || PICP_LITE1) s_lite = pose_lite(pr, pt);
         s_done = o.done;
         if (o.done) store_state(&s_st, pr, pt, chi_prev, o, round);
       }
@@ -551,17 +524,7 @@ static int s4_bs() {
   }();
   return bs;
 }
-// Split 1 and 2 (one block per CU): 512 threads (two waves per SIMD, <= 256 VGPRs, up to eight
-// register items per lane) or 1024 threads (four waves per SIMD, <= 128 VGPRs: MINW 4, up to four
-// register items per lane) -- PICP_BLOCK_BS=1024 (A/B).
-static int wide_bs() {
-  static const int bs = [] {
-    const char* e = getenv("PICP_BLOCK_BS");
-    return (e && atoi(e) == 1024) ? 1024 : PICP_BBLOCK;
-  }();
-  return bs;
-}
-extern "C" int picp_block_threads(int split) { return (split == 4) ? s4_bs() : wide_bs(); }
+extern "C" int picp_block_threads(int split) { return (split == 4) ? s4_bs() : PICP_BBLOCK; }
 
 // dynamic LDS of a launch: the part of a problem (or of its 1/split share) past the
 // register-resident npt x BS items, capped by the stage
@@ -587,10 +550,6 @@ static const void* block_kernel_nbw(int var) {
 template <int N>
 static const void* block_kernel_n(int var, int bs, int split) {
   if (bs == 256) return block_kernel_nbw<N, 256, 2>(var);
-  if (bs == 1024) {
-    if constexpr (N <= 4) return block_kernel_nbw<N, 1024, 4>(var);  // <= 128 VGPRs: NPT <= 4
-    return nullptr;
-  }
   if (split == 4) {
     if constexpr (N <= 4) return block_kernel_nbw<N, 512, 4>(var);  // <= 128 VGPRs: NPT <= 4
     return nullptr;
@@ -608,11 +567,8 @@ static const void* block_kernel_ptr(int npt, int var, int bs, int split) {
   }
 }
 
-// Register items per lane the 128-VGPR layouts allow (split 4 with 512 threads, 1024-thread
-// blocks); 8 otherwise.
-extern "C" int picp_block_npt_cap(int split) {
-  return ((split == 4 && s4_bs() == 512) || (split != 4 && wide_bs() == 1024)) ? 4 : 8;
-}
+// Register items per lane the split-4 512-thread layout allows (its 128-VGPR budget); 8 otherwise.
+extern "C" int picp_block_npt_cap(int split) { return (split == 4 && s4_bs() == 512) ? 4 : 8; }
 
 // Blocks of the variants a launch with these arguments may use that one CU holds at once (the
 // hardware limit from registers, LDS and waves; other work on the device is not counted; the

@@ -40,44 +40,26 @@ struct Acc {
   float chi_in, chi_out;
 };
 
-// n_in / n_proj of a wave, counted on the scalar unit (default): s_bcnt1 + s_add per predicate mask
-// (the compiler still spends a v_cndmask + v_cmp_ne per ballot).  Inside a divergent loop the
-// counter is kept per lane: lane 0 of a wave runs every iteration any lane of it runs (its items
-// come first), so wave_counts reads lane 0.  -DPICP_LANE_COUNTS=1 (A/B): per-lane counters
-// (`c += pred`, about one VALU instruction per count) summed over the wave once per round; measured
-// far slower (C4 23.9M vs 29.3M it/s, C2 201k vs 220k, profiles/r04/lite/).
-#ifndef PICP_LANE_COUNTS
-#define PICP_LANE_COUNTS 0
-#endif
+// n_in / n_proj of a wave, counted on the SCALAR unit: each item's inlier and projectable
+// predicates are already lane masks (v_cmp results), so a count is s_bcnt1 + s_add per mask,
+// issued beside the VALU work instead of as selects and adds in it.  Inside a divergent loop the
+// compiler keeps the counter per lane; a lane's copy then counts the items of every iteration
+// that lane ran, and lane 0 of a wave runs every iteration any lane of it runs (its items come
+// first), so wave_counts reads lane 0.
 struct Cnt {
   unsigned n_in, n_proj;
 };
 
 __device__ __forceinline__ void cnt_add(Cnt& c, bool inl, bool valid) {
-#if PICP_LANE_COUNTS
-  c.n_in += inl ? 1u : 0u;
-  c.n_proj += valid ? 1u : 0u;
-#else
   c.n_in += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(inl));
   c.n_proj += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(valid));
-#endif
 }
 
 // After wave_reduce32 (lane l holds the wave total of value l >> 1): the wave's counts, as the
 // float words of PICP_P_N_IN / PICP_P_N_PROJ (exact: a wave counts far fewer than 2^24 items).
-// Every lane of the wave must be active (after the item loops have reconverged).
 __device__ __forceinline__ float wave_counts(float wsum, int lane, const Cnt& c) {
-#if PICP_LANE_COUNTS
-  unsigned n_in = c.n_in, n_proj = c.n_proj;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    n_in += (unsigned)__shfl_xor((int)n_in, o);
-    n_proj += (unsigned)__shfl_xor((int)n_proj, o);
-  }
-#else
   const unsigned n_in = __builtin_amdgcn_readlane(c.n_in, 0);
   const unsigned n_proj = __builtin_amdgcn_readlane(c.n_proj, 0);
-#endif
   wsum = ((lane >> 1) == PICP_P_N_IN) ? (float)n_in : wsum;
   return ((lane >> 1) == PICP_P_N_PROJ) ? (float)n_proj : wsum;
 }
@@ -253,9 +235,7 @@ __device__ __forceinline__ float item_depth(const Pose& T, float x, float y, flo
 
 // RCP: RCP_DIV (the IEEE division) or RCP_FAST (rcp_rn: the caller's wave vote found the depth
 // inside rcp_safe's range; the same bits).
-// LITE: accumulate_pinhole2's LITE precondition holds; a skipped item then gets iz and e zeroed
-// with no wave vote (straight-line code across the items of a lane).
-template <bool KEEP, int RCP = RCP_DIV, bool LITE = false>
+template <bool KEEP, int RCP = RCP_DIV>
 __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, float thr,
                                                    float inv_thr, float x, float y,
                                                    float z, float u, float v, bool in_range,
@@ -294,11 +274,7 @@ __device__ __forceinline__ void accumulate_pinhole(const Pose& T, const Cam& C, 
   // J is exactly 0 once iz alone is zeroed, and fma(+-0, finite, h) == h exactly (the sums start
   // at +0 and never become -0), so waves without a dangerous skipped point zero only iz, with
   // bit-identical H and b.
-  if constexpr (LITE) {
-    iz = use ? iz : 0.0f;
-    e0 = use ? e0 : 0.0f;
-    e1 = use ? e1 : 0.0f;
-  } else if (__all(use | (proj & (pc2 >= 1e-12f) & (chi <= FLT_MAX)))) {
+  if (__all(use | (proj & (pc2 >= 1e-12f) & (chi <= FLT_MAX)))) {
     iz = use ? iz : 0.0f;
   } else {
     iz = use ? iz : 0.0f;
@@ -467,12 +443,7 @@ __device__ __forceinline__ bool pair_rcp_safe(const Pose& T, f2 x, f2 y, f2 z) {
   return rcp_safe(d.x) & rcp_safe(d.y);
 }
 
-// LITE: the caller guarantees (lite_bounds, taken once per set of items and per pose) that every
-// item's pc and ph are finite: each coordinate |x|, |y|, |z| <= 1e30 and the pose and K entries
-// bounded, so |pc| < 1e31 and |ph| < 1e38.  A skipped item then needs only iz and e zeroed: its J
-// (every term a product with iz, iz^2 or a J entry) is +-0 and adds nothing to H or b (the sums
-// never become -0 unless every term is zero), 5 selects per item fewer than zeroing all 8 inputs.
-template <bool KEEP, int RCP = RCP_CHECK, bool LITE = false>
+template <bool KEEP, int RCP = RCP_CHECK>
 __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C, float thr,
                                                     float inv_thr, f2 x, f2 y, f2 z,
                                                     f2 u, f2 v, bool inA, bool inB, Acc2& a, Cnt& n) {
@@ -519,11 +490,7 @@ __device__ __forceinline__ void accumulate_pinhole2(const Pose& T, const Cam& C,
   // these selects for waves of projectable items, as accumulate_pinhole does, measured 1-4 %
   // slower here: the branches split the unrolled pairs' straight-line schedule.)
 #define PICP_Z2(val) val = (f2){useA ? val.x : 0.0f, useB ? val.y : 0.0f}
-  if constexpr (LITE) {
-    PICP_Z2(iz); PICP_Z2(e0); PICP_Z2(e1);
-  } else {
-    PICP_Z2(iz); PICP_Z2(pc0); PICP_Z2(pc1); PICP_Z2(pc2); PICP_Z2(ph0); PICP_Z2(ph1); PICP_Z2(e0); PICP_Z2(e1);
-  }
+  PICP_Z2(iz); PICP_Z2(pc0); PICP_Z2(pc1); PICP_Z2(pc2); PICP_Z2(ph0); PICP_Z2(ph1); PICP_Z2(e0); PICP_Z2(e1);
 #undef PICP_Z2
   f2 J0[6], J1[6];
   {
@@ -665,60 +632,14 @@ __device__ __forceinline__ void accumulate_general2(const Pose& T, const Cam& C,
 
 // PH: the per-item variant (PICP_V_*); keep is read only by the general variant; RCP: how the
 // pinhole variants take the reciprocal (RCP_*)
-template <int PH, int RCP = RCP_CHECK, bool LITE = false>
+template <int PH, int RCP = RCP_CHECK>
 __device__ __forceinline__ void accumulate2(const Pose& T, const Cam& C, float thr, float inv_thr,
                                             bool keep, f2 x, f2 y, f2 z, f2 u, f2 v, bool inA,
                                             bool inB, Acc2& a, Cnt& n) {
   if constexpr (PH == PICP_V_GENERAL)
     accumulate_general2(T, C, thr, keep, x, y, z, u, v, inA, inB, a, n);
   else
-    accumulate_pinhole2<PH == PICP_V_PINHOLE_KEEP, RCP, LITE>(T, C, thr, inv_thr, x, y, z, u, v, inA, inB, a, n);
-}
-
-// LITE in the one-slot form (accumulate_regs1 / accumulate_stream1) only with -DPICP_LITE1=1: alone
-// it is 3-8 % faster (tools/ubench/lin_ubench.hip), but in the 128-VGPR split-4 kernel the second
-// copy of the item loop spilled (C4 at 128 frames 17.7M vs 21.5M it/s) and C5 lost 3 %
-// (profiles/r04/lite/).
-#ifndef PICP_LITE1
-#define PICP_LITE1 0
-#endif
-// accumulate_pinhole2's LITE precondition, in three parts: coords_lite, an item's coordinates (NaN
-// fails), taken once when the items are loaded; cam_lite, K, once per launch; pose_lite, the
-// round's pose, taken by the thread that writes it to LDS (an LDS flag beside the pose: every wave
-// checking the pose itself cost ~40 VALU instructions per wave and round).  -DPICP_LITE=0 (A/B)
-// never takes the LITE form.
-#ifndef PICP_LITE
-#define PICP_LITE 1
-#endif
-// A wave-uniform flag as a scalar: branches on it compile to a scalar branch that skips the other
-// form (on a per-lane bool the compiler emits an exec-masked if/else whose untaken side still
-// issues when its mask is empty).
-__device__ __forceinline__ bool wave_uniform(bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
-
-__device__ __forceinline__ bool coords_lite(float x, float y, float z) {
-  return (fabsf(x) <= 1e30f) & (fabsf(y) <= 1e30f) & (fabsf(z) <= 1e30f);
-}
-
-// the pose words (R column-major 0-8, t 9-11) within LITE's bounds, as one lane holding word w
-// (w < 12) tests it; every lane of a wave then takes __all
-__device__ __forceinline__ bool pose_word_lite(int w, float v) {
-  return PICP_LITE && (w >= 12 || fabsf(v) <= (w < 9 ? 2.0f : 1e30f));  // a comparison with NaN is false
-}
-
-// the whole pose, by one thread (the pose's writer, once per round)
-__device__ __forceinline__ bool pose_lite(const float* pr, const float* pt) {
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) ok &= pose_word_lite(i, pr[i]);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) ok &= pose_word_lite(9 + i, pt[i]);
-  return ok;
-}
-
-// K's entries the pinhole path multiplies, within LITE's bounds (once per launch)
-__device__ __forceinline__ bool cam_lite(const Cam& C) {
-  return PICP_LITE && (fabsf(C.k00) <= 1e6f) & (fabsf(C.k02) <= 1e6f) & (fabsf(C.k11) <= 1e6f) &
-                          (fabsf(C.k12) <= 1e6f);
+    accumulate_pinhole2<PH == PICP_V_PINHOLE_KEEP, RCP>(T, C, thr, inv_thr, x, y, z, u, v, inA, inB, a, n);
 }
 
 // NPT register-resident items per lane (item k at lane + k * stride) as pairs (k, k + 1) (NPT == 1:
@@ -726,13 +647,11 @@ __device__ __forceinline__ bool cam_lite(const Cam& C) {
 // instead of one per pair: the pairs then run as one straight-line block (a vote per pair split
 // them into blocks, so every per-item predicate crossing the block edge was kept as a 0/1 VGPR and
 // compared again, and the masks' scalar registers spilled).
-// lite: accumulate_pinhole2's LITE precondition holds for this wave's items and pose (wave-uniform).
 template <int PH, int NPT>
 __device__ __forceinline__ void accumulate_regs(const Pose& T, const Cam& C, float thr, float inv_thr,
                                                 bool keep, const float* xs, const float* ys,
                                                 const float* zs, const float* us, const float* vs,
-                                                int first, int stride, int n, Acc2& a, Cnt& cnt,
-                                                bool lite = false) {
+                                                int first, int stride, int n, Acc2& a, Cnt& cnt) {
   bool fast = true;
   if constexpr (PH != PICP_V_GENERAL) {
 #pragma unroll
@@ -741,24 +660,20 @@ __device__ __forceinline__ void accumulate_regs(const Pose& T, const Cam& C, flo
       fast &= pair_rcp_safe(T, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]}, (f2){zs[k], zs[k1]});
     }
   }
-  auto run = [&](auto rcp, auto lt) {
+  auto run = [&](auto rcp) {
 #pragma unroll
     for (int k = 0; k < NPT; k += 2) {
       const int k1 = (k + 1 < NPT) ? k + 1 : k;
-      accumulate2<PH, decltype(rcp)::value, decltype(lt)::value>(
-          T, C, thr, inv_thr, keep, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]}, (f2){zs[k], zs[k1]},
-          (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]}, first + k * stride < n,
-          k + 1 < NPT && first + (k + 1) * stride < n, a, cnt);
+      accumulate2<PH, decltype(rcp)::value>(T, C, thr, inv_thr, keep, (f2){xs[k], xs[k1]}, (f2){ys[k], ys[k1]},
+                                            (f2){zs[k], zs[k1]}, (f2){us[k], us[k1]}, (f2){vs[k], vs[k1]},
+                                            first + k * stride < n, k + 1 < NPT && first + (k + 1) * stride < n,
+                                            a, cnt);
     }
   };
-  if (PH == PICP_V_GENERAL || __all(fast)) {
-    if (PH != PICP_V_GENERAL && lite)
-      run(std::integral_constant<int, RCP_FAST>(), std::true_type());
-    else
-      run(std::integral_constant<int, RCP_FAST>(), std::false_type());
-  } else {
-    run(std::integral_constant<int, RCP_DIV>(), std::false_type());
-  }
+  if (PH == PICP_V_GENERAL || __all(fast))
+    run(std::integral_constant<int, RCP_FAST>());
+  else
+    run(std::integral_constant<int, RCP_DIV>());
 }
 
 // Which accumulation form a kernel with NPT register-resident items per lane uses.  Measured on
@@ -792,8 +707,7 @@ template <int PH, int NPT>
 __device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, float thr, float inv_thr,
                                                  bool keep, const float* xs, const float* ys,
                                                  const float* zs, const float* us, const float* vs,
-                                                 int first, int stride, int n, Acc& a, Cnt& cnt,
-                                                 bool lite = false) {
+                                                 int first, int stride, int n, Acc& a, Cnt& cnt) {
   if constexpr (PH == PICP_V_GENERAL) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k)
@@ -802,10 +716,9 @@ __device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, fl
     bool fast = true;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) fast &= rcp_safe(item_depth(T, xs[k], ys[k], zs[k]));
-    auto run = [&](auto rcp, auto lt) {
+    auto run = [&](auto rcp) {
       constexpr bool KP = PH == PICP_V_PINHOLE_KEEP;
       constexpr int R = decltype(rcp)::value;
-      constexpr bool LT = decltype(lt)::value;
 #if PICP_P1
       // items in pairs (k, k + 1) through accumulate_pinhole_p1: the same sums in the same order
       // as item by item, with two dependency chains through the per-item math
@@ -830,24 +743,20 @@ __device__ __forceinline__ void accumulate_regs1(const Pose& T, const Cam& C, fl
         // SIMDs in turn every SIMD then issues one slot less when n <= (NPT - 1/2) x BS (C5's
         // ~1,750 correspondences on 2,048 slots).  A skipped item adds exact zeros: same bits.
         if (NPT < 2 || k + 1 < NPT || __any(first + k * stride < n))
-          accumulate_pinhole<KP, R, LT>(T, C, thr, inv_thr, xs[k], ys[k], zs[k], us[k], vs[k],
-                                        first + k * stride < n, a, cnt);
+          accumulate_pinhole<KP, R>(T, C, thr, inv_thr, xs[k], ys[k], zs[k], us[k], vs[k], first + k * stride < n, a,
+                                    cnt);
 #endif
     };
-    if (__all(fast)) {
-      if (lite)
-        run(std::integral_constant<int, RCP_FAST>(), std::true_type());
-      else
-        run(std::integral_constant<int, RCP_FAST>(), std::false_type());
-    } else {
-      run(std::integral_constant<int, RCP_DIV>(), std::false_type());
-    }
+    if (__all(fast))
+      run(std::integral_constant<int, RCP_FAST>());
+    else
+      run(std::integral_constant<int, RCP_DIV>());
   }
 }
 
 // One streamed (LDS or HBM) item, pinhole or general, the fast reciprocal by a vote of the lanes
 // that run this item (the loops that call it are divergent).
-template <int PH, bool LITE = false>
+template <int PH>
 __device__ __forceinline__ void accumulate_item(const Pose& T, const Cam& C, float thr, float inv_thr,
                                                 bool keep, float x, float y, float z, float u, float v,
                                                 bool in_range, Acc& a, Cnt& n) {
@@ -855,8 +764,7 @@ __device__ __forceinline__ void accumulate_item(const Pose& T, const Cam& C, flo
     accumulate_one(T, C, thr, keep, x, y, z, u, v, in_range, a, n);
   } else {
     if (__all(rcp_safe(item_depth(T, x, y, z))))
-      accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_FAST, LITE>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a,
-                                                                    n);
+      accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_FAST>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
     else
       accumulate_pinhole<PH == PICP_V_PINHOLE_KEEP, RCP_DIV>(T, C, thr, inv_thr, x, y, z, u, v, in_range, a, n);
   }
@@ -865,7 +773,7 @@ __device__ __forceinline__ void accumulate_item(const Pose& T, const Cam& C, flo
 // Streamed (LDS or HBM) items i, i + stride, i + 2 stride, ... (i = first) of one lane into one
 // slot, in that order: pairs through accumulate_pinhole_p1 (the fast reciprocal by a vote of the
 // lanes that run the pair), the general variant item by item.  get(i, x, y, z, u, v) loads item i.
-template <int PH, bool LITE = false, typename Get>
+template <int PH, typename Get>
 __device__ __forceinline__ void accumulate_stream1(const Pose& T, const Cam& C, float thr, float inv_thr, bool keep,
                                                    int first, int stride, int count, Get get, Acc& a, Cnt& n) {
 #if PICP_P1
@@ -889,7 +797,7 @@ __device__ __forceinline__ void accumulate_stream1(const Pose& T, const Cam& C, 
   for (int i = first; i < count; i += stride) {
     float x, y, z, u, v;
     get(i, x, y, z, u, v);
-    accumulate_item<PH, LITE>(T, C, thr, inv_thr, keep, x, y, z, u, v, true, a, n);
+    accumulate_item<PH>(T, C, thr, inv_thr, keep, x, y, z, u, v, true, a, n);
   }
 }
 

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(PICP_BLOCK) void picp_round_kernel(
 
   Acc2 a;
   acc2_zero(a);
-  Cnt nc = {0u, 0u};  // the counts (picp_device.h cnt_add: per lane, or per wave in lane 0)
+  Cnt nc = {0u, 0u};  // the wave's counts; the loop is divergent at the tail: lane 0's copy is the total
   for (int c = c0; c < count; c += RING * STEP) {
 #pragma unroll
     for (int sl = 0; sl < RING; ++sl) {

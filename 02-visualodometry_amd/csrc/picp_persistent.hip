@@ -39,22 +39,8 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #ifndef PICP_POSE_STAGGER
 #define PICP_POSE_STAGGER 8
 #endif
-// -DPICP_POSE_BACKOFF=M (A/B, 10-ns ticks; 0 off): a follower sleeps through the first part of its
-// pose wait -- the previous round's wait less M -- so that the followers' polls do not crowd the
-// pose's line while the leader sweeps the partials and solves.  A wait that overslept the pose
-// measures sleep + one poll, so with M above one poll's latency the next sleep shrinks until the
-// polls start before the pose lands again.
-#ifndef PICP_POSE_BACKOFF
-#define PICP_POSE_BACKOFF 0
-#endif
 #ifndef PICP_POSE_NPOLL  // polls in flight in the followers' pose wait (2 or 3), when staggered
 #define PICP_POSE_NPOLL 2
-#endif
-// One item per lane (C2): through accumulate (default: the IEEE division and the per-item zeroing
-// vote) or accumulate_regs1 (-DPICP_SCALAR_REGS1=1: the fast reciprocal by one vote and the LITE
-// zeroing; measured no faster, 205-211k vs 211-219k it/s, profiles/r04/lite/)
-#ifndef PICP_SCALAR_REGS1
-#define PICP_SCALAR_REGS1 0
 #endif
 #define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
@@ -105,7 +91,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   __shared__ float s_tot[PICP_NPART];
   __shared__ float s_wave[BS / 64][PICP_NPART];
   __shared__ float s_pose[12];
-  __shared__ int s_lite;  // s_pose within accumulate_pinhole2's LITE bounds (set with s_pose)
   __shared__ int s_done;
   __shared__ int s_tmo;  // a wait of this block timed out (the error word is for the host)
 
@@ -156,7 +141,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
     for (int i = 0; i < 9; ++i) s_pose[i] = s.R[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
-    s_lite = (acc_pairs(NPT) || PICP_LITE1) && pose_lite(s.R, s.t);
     s_done = s.done;
     s_tmo = 0;
     if (leader && s.done) st_out[p] = s;
@@ -172,16 +156,9 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   const float thr = A.threshold;
   const float inv_thr = 1.0f / thr;
   const bool keep = A.keep_outliers != 0;
-  // the wave's register items all within accumulate_pinhole2's LITE bounds (checked once)
-  bool items_ok = acc_pairs(NPT) || PICP_LITE1;  // LITE: the pair form (picp_device.h)
-#pragma unroll
-  for (int k = 0; k < NPT; ++k) items_ok &= coords_lite(xs[k], ys[k], zs[k]);
-  // per wave: the items a lane checked are the ones it linearizes
-  const bool items_lite = __all(items_ok) && cam_lite(C);
 
   float chi_prev = FLT_MAX;  // the leader's loop state besides the pose (exec/icp_test.cpp:89)
   unsigned long long pose_sink = 0, pa = 0, pb = 0, pc = 0;  // the follower's pose polls (PICP_POSE_STAGGER)
-  unsigned long long backoff = 0;  // the follower's sleep before polling (PICP_POSE_BACKOFF)
   for (unsigned epoch = 1; !s_done; ++epoch) {
     // every wait of this round is bounded from the round's start (a whole solve may take far
     // longer than timeout_ticks at large max_rounds; one round never does)
@@ -194,7 +171,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
     T.r02 = s_pose[6]; T.r12 = s_pose[7]; T.r22 = s_pose[8];
     T.t0 = s_pose[9]; T.t1 = s_pose[10]; T.t2 = s_pose[11];
     float v[PICP_NPART];
-    Cnt nc = {0u, 0u};  // n_in / n_proj (picp_device.h cnt_add)
+    Cnt nc = {0u, 0u};  // the wave's n_in / n_proj (scalar unit)
     if constexpr (NPT == 1) {  // one item per lane: the scalar path (latency-bound C2 frames)
       Acc a;
 #pragma unroll
@@ -202,13 +179,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
 #pragma unroll
       for (int i = 0; i < 6; ++i) a.b[i] = 0.0f;
       a.chi_in = a.chi_out = 0.0f;
-#if PICP_SCALAR_REGS1
-      // the fast reciprocal by one wave vote and the LITE zeroing (accumulate_regs1)
-      accumulate_regs1<PH, 1>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc,
-                              wave_uniform(items_lite && s_lite != 0));
-#else
       accumulate<PH>(T, C, thr, inv_thr, keep, xs[0], ys[0], zs[0], us[0], vs[0], tid < count, a, nc);
-#endif
 #pragma unroll
       for (int i = 0; i < 21; ++i) v[PICP_P_H + i] = a.h[i];
 #pragma unroll
@@ -222,14 +193,12 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
       if constexpr (acc_pairs(NPT)) {
         Acc2 a;
         acc2_zero(a);
-        accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc,
-                                 wave_uniform(items_lite && s_lite != 0));
+        accumulate_regs<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc);
         acc2_fold(a, v);
       } else {
         Acc a;
         acc_zero(a);
-        accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc,
-                                  PICP_LITE1 && wave_uniform(items_lite && s_lite != 0));
+        accumulate_regs1<PH, NPT>(T, C, thr, inv_thr, keep, xs, ys, zs, us, vs, tid, BS, count, a, nc);
         acc_fold(a, v);
       }
     }
@@ -349,7 +318,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
             for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];
 #pragma unroll
         for (int i = 0; i < 3; ++i) s_pose[9 + i] = pt[i];
-            if constexpr (acc_pairs(NPT) || PICP_LITE1) s_lite = pose_lite(pr, pt);
             s_done = o.done;
             if (o.done) {
               store_state(st_out + p, pr, pt, chi_prev, o, (int)epoch);
@@ -379,13 +347,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         auto good = [&](unsigned long long v) { return __all((unsigned)(v >> 32) == tbase + epoch); };
         pose_sink ^= pa ^ pb ^ pc;  // last round's polls: long complete
         bool tmo = false;
-#if PICP_POSE_BACKOFF
-        const unsigned long long t_wait = __builtin_amdgcn_s_memrealtime();
-        if (backoff > 0) {
-          const unsigned long long until = t_wait + backoff;
-          while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(2);
-        }
-#endif
         pa = poll();
         __builtin_amdgcn_s_sleep(PICP_POSE_STAGGER);
         if constexpr (PICP_POSE_NPOLL >= 3) {
@@ -414,13 +375,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           gp = lane == 12 ? 1u : 0u;  // force done
           if (lane < 12) gp = __float_as_uint(s_pose[lane]);
         }
-#if PICP_POSE_BACKOFF
-        {
-          const unsigned long long waited = __builtin_amdgcn_s_memrealtime() - t_wait;
-          backoff = (waited > PICP_POSE_BACKOFF) ? waited - PICP_POSE_BACKOFF : 0ull;
-          backoff = backoff < 2000ull ? backoff : 2000ull;  // at most 20 us
-        }
-#endif
 #else
         for (;;) {
           bool ok = true;
@@ -440,10 +394,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
 #endif
         if (lane < 12) s_pose[lane] = __uint_as_float((unsigned)gp);
         if (lane == 12) s_done = (int)(unsigned)gp;
-        if constexpr (acc_pairs(NPT) || PICP_LITE1) {
-          const bool pl = __all(pose_word_lite(lane, __uint_as_float((unsigned)gp)));
-          if (lane == 0) s_lite = pl;
-        }
       }
       __syncthreads();
       PSTAMP(2);

@@ -15,7 +15,7 @@
 #include "picp_device.h"
 using namespace picp;
 
-template <int NPT, bool PAIRS, int BS, bool LITE = false>
+template <int NPT, bool PAIRS, int BS>
 __global__ __launch_bounds__(BS) void lin(const float* __restrict__ X, const float* __restrict__ Y,
                                           const float* __restrict__ Z, const float* __restrict__ U,
                                           const float* __restrict__ V, int n, int rounds, float* sink) {
@@ -48,14 +48,12 @@ __global__ __launch_bounds__(BS) void lin(const float* __restrict__ X, const flo
     if constexpr (PAIRS) {
       Acc2 a;
       acc2_zero(a);
-      accumulate_regs<PICP_V_PINHOLE, NPT>(T, C, thr, inv_thr, false, xs, ys, zs, us, vs, tid, BS, count, a, nc,
-                                           LITE);
+      accumulate_regs<PICP_V_PINHOLE, NPT>(T, C, thr, inv_thr, false, xs, ys, zs, us, vs, tid, BS, count, a, nc);
       acc2_fold(a, v);
     } else {
       Acc a;
       acc_zero(a);
-      accumulate_regs1<PICP_V_PINHOLE, NPT>(T, C, thr, inv_thr, false, xs, ys, zs, us, vs, tid, BS, count, a, nc,
-                                            LITE);
+      accumulate_regs1<PICP_V_PINHOLE, NPT>(T, C, thr, inv_thr, false, xs, ys, zs, us, vs, tid, BS, count, a, nc);
       acc_fold(a, v);
     }
     const float wsum = wave_counts(wave_reduce32(v, lane), lane, nc);
@@ -67,7 +65,7 @@ __global__ __launch_bounds__(BS) void lin(const float* __restrict__ X, const flo
   if (tid == 0) sink[blockIdx.x] = check;
 }
 
-template <int NPT, bool PAIRS, int BS, bool LITE = false>
+template <int NPT, bool PAIRS, int BS>
 static void run(const char* name, float* const* d, int n_per_cu, int cus, int rounds, float* sink) {
   const int per_block = NPT * BS;
   const int blocks = cus * (n_per_cu / per_block);
@@ -75,9 +73,9 @@ static void run(const char* name, float* const* d, int n_per_cu, int cus, int ro
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  hipLaunchKernelGGL((lin<NPT, PAIRS, BS, LITE>), dim3(blocks), dim3(BS), 0, 0, d[0], d[1], d[2], d[3], d[4], n, 4, sink);
+  hipLaunchKernelGGL((lin<NPT, PAIRS, BS>), dim3(blocks), dim3(BS), 0, 0, d[0], d[1], d[2], d[3], d[4], n, 4, sink);
   hipEventRecord(e0, 0);
-  hipLaunchKernelGGL((lin<NPT, PAIRS, BS, LITE>), dim3(blocks), dim3(BS), 0, 0, d[0], d[1], d[2], d[3], d[4], n, rounds, sink);
+  hipLaunchKernelGGL((lin<NPT, PAIRS, BS>), dim3(blocks), dim3(BS), 0, 0, d[0], d[1], d[2], d[3], d[4], n, rounds, sink);
   hipEventRecord(e1, 0);
   hipEventSynchronize(e1);
   float ms = 0.0f;
@@ -115,19 +113,14 @@ int main(int argc, char** argv) {
 #else
   printf("build: no packed FP32 (shipped)\n");
 #endif
-  // one 512-thread block per CU, 4096 items per block (C3: 245 blocks x 4082); LITE: the zeroing
-  // of iz and e only (picp_device.h accumulate_pinhole2 / accumulate_pinhole)
-  for (int rep = 0; rep < 2; ++rep) {
-    run<8, true, 512>("NPT 8, pairs, 512 thr, 1 blk/CU", d, 4096, cus, rounds, sink);
-    run<8, true, 512, true>("NPT 8, pairs, LITE", d, 4096, cus, rounds, sink);
-    run<8, false, 512>("NPT 8, one slot, 512 thr, 1 blk/CU", d, 4096, cus, rounds, sink);
-    run<8, false, 512, true>("NPT 8, one slot, LITE", d, 4096, cus, rounds, sink);
-    // the same items per CU as two blocks of NPT 4 (needs <= 128 VGPRs to be co-resident)
-    run<4, false, 512>("NPT 4, one slot, 512 thr, 2 blk/CU", d, 4096, cus, rounds, sink);
-    run<4, false, 512, true>("NPT 4, one slot, LITE", d, 4096, cus, rounds, sink);
-    run<1, false, 512>("NPT 1, one slot, 512 thr, 8 blk/CU", d, 4096, cus, rounds, sink);
-    run<1, false, 512, true>("NPT 1, one slot, LITE", d, 4096, cus, rounds, sink);
-  }
+  // one 512-thread block per CU, 4096 items per block (C3: 245 blocks x 4082)
+  run<8, true, 512>("NPT 8, pairs, 512 thr, 1 blk/CU", d, 4096, cus, rounds, sink);
+  run<8, false, 512>("NPT 8, one slot, 512 thr, 1 blk/CU", d, 4096, cus, rounds, sink);
+  // the same items per CU as two blocks of NPT 4 (needs <= 128 VGPRs to be co-resident)
+  run<4, true, 512>("NPT 4, pairs, 512 thr, 2 blk/CU", d, 4096, cus, rounds, sink);
+  run<4, false, 512>("NPT 4, one slot, 512 thr, 2 blk/CU", d, 4096, cus, rounds, sink);
+  run<2, false, 512>("NPT 2, one slot, 512 thr, 4 blk/CU", d, 4096, cus, rounds, sink);
+  run<4, false, 1024>("NPT 4, one slot, 1024 thr, 1 blk/CU", d, 4096, cus, rounds, sink);
   hipDeviceSynchronize();
   return 0;
 }
