@@ -2,7 +2,9 @@
 # Round-4 profiles at HEAD: rocprofv3 kernel-trace/stats per bench workload (C2, C3, C4 at 1024 and
 # at the 128-frame per-rank shape, C5, the 16M streaming frame), then the HBM traffic counters
 # FETCH_SIZE and WRITE_SIZE in SEPARATE --pmc passes (MI355X_MICROARCH.md), and one SQ pass
-# (VALU instructions, waves, busy cycles) for the VALU-bound kernels.  Every step time-limited;
+# (VALU instructions, waves, busy cycles) for the VALU-bound kernels.  Each trace also gets a
+# trace_summary_<workload>.json: the dominant kernel's mean over every dispatch and over the timed
+# ones (tools/trace_summary.py).  Every step time-limited;
 # stop at the first failure.  OUT=${OUT:-gpurun_out/r04/prof}
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/r04/prof}
@@ -15,9 +17,13 @@ args() {  # workload tag -> bench arguments
   esac
 }
 for W in ${WLS:-c2 c3 c4 c4x128 c5 c2n16m}; do
-  A="--no-cpu --skip-extras --steps 10 --warmup 2 --samples 1 $(args $W)"
+  # warm-up long enough for the clocks to settle (C4's first launches run up to 13 % longer)
+  A="--no-cpu --skip-extras --steps 10 --warmup ${TRACE_WARMUP:-10} --samples 1 $(args $W)"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/${W}_trace -o run --output-format csv -- python3 bench.py $A > $OUT/${W}_trace.log 2>&1 || { echo "trace $W failed"; tail $OUT/${W}_trace.log; exit 1; }
   cp $OUT/${W}_trace/run_kernel_stats.csv $OUT/kernel_stats_$W.csv
+  case $W in c5) KP="_Z22picp_match" ;; c2n16m) KP="void picp_round" ;; *) KP="void picp_" ;; esac
+  T=10; [ $W = c5 ] && T=0
+  python3 tools/trace_summary.py $OUT/${W}_trace/run_kernel_trace.csv "$KP" $T $OUT/${W}_trace.log > $OUT/trace_summary_$W.json
   python3 -c "import json; d=json.loads([l for l in open('$OUT/${W}_trace.log').read().splitlines() if l.startswith('{')][-1]); print('$W', d['value'], d['unit'], d['ms_per_step'])"
 done
 for P in ${PMCS:-c2:c2_persistent:picp_persistent c3:c3_persistent:picp_persistent c4:c4x1024_block:picp_block c4x128:c4x128:picp_ c2n16m:stream16m:picp_round_kernel}; do
