@@ -42,6 +42,11 @@ using namespace picp;
 #else
 #define PICP_BPOLL_PAUSE() ((void)0)
 #endif
+// The split exchange's poll: every partner's granules loaded before any is checked (default), or
+// partner by partner (-DPICP_XG_BATCH=0, round 3's form; A/B).
+#ifndef PICP_XG_BATCH
+#define PICP_XG_BATCH 1
+#endif
 #define PICP_XG 64            // exchange granules per block per round: 32 hi + 32 lo
 
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
@@ -451,6 +456,29 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
         }
         part_t[h & 3] = (double)hi + (double)lo;
         for (;;) {
+#if PICP_XG_BATCH
+          // every partner's two granules loaded before any tag is checked (the partners are a
+          // block-uniform set, so the loads issue back to back): one round trip per poll.  Checking
+          // each partner right after its loads (PICP_XG_BATCH=0) waited one round trip per
+          // partner, three per poll at split 4.
+          unsigned long long gh[4], gl[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            gh[q] = gl[q] = 0ull;
+            if (q < split && q != h) {
+              const bgu64_t* theirs = xgg + (slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * PICP_XG;
+              gh[q] = __hip_atomic_load(theirs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              gl[q] = __hip_atomic_load(theirs + PICP_NPART + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if ((pending & (1u << q)) && (unsigned)(gh[q] >> 32) == tag && (unsigned)(gl[q] >> 32) == tag) {
+              part_t[q] = (double)__uint_as_float((unsigned)gh[q]) + (double)__uint_as_float((unsigned)gl[q]);
+              pending &= ~(1u << q);
+            }
+          }
+#else
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (!(pending & (1u << q))) continue;
@@ -463,6 +491,7 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
               pending &= ~(1u << q);
             }
           }
+#endif
           if (!pending) break;
           if (__builtin_amdgcn_s_memrealtime() > deadline) {
             __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

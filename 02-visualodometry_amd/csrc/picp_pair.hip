@@ -299,15 +299,22 @@ __global__ __launch_bounds__(PP_BS) void picp_pair_kernel(
         }
         part_t[h & 3] = (double)hi + (double)lo;
         for (;;) {
+          // every partner's granules loaded before any tag is checked: one round trip per poll
+          // (picp_block.hip PICP_XG_BATCH)
+          unsigned long long gh[4], gl[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (!(pending & (1u << q))) continue;
-            const pgu64_t* theirs = xgg + ((slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * 2 + f) * PP_XG;
-            const unsigned long long gh = __hip_atomic_load(theirs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long gl =
-                __hip_atomic_load(theirs + PICP_NPART + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) {
-              part_t[q] = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
+            gh[q] = gl[q] = 0ull;
+            if (q < split && q != h) {
+              const pgu64_t* theirs = xgg + ((slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * 2 + f) * PP_XG;
+              gh[q] = __hip_atomic_load(theirs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              gl[q] = __hip_atomic_load(theirs + PICP_NPART + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if ((pending & (1u << q)) && (unsigned)(gh[q] >> 32) == tag && (unsigned)(gl[q] >> 32) == tag) {
+              part_t[q] = (double)__uint_as_float((unsigned)gh[q]) + (double)__uint_as_float((unsigned)gl[q]);
               pending &= ~(1u << q);
             }
           }
