@@ -34,6 +34,8 @@
 //   victims 17-22: a 32-bit VALU write of one half of a register pair, then a packed-FP32 read
 //             of the pair after 0 / 1 / 2 wait states (inline asm, explicit v200-v205): 17/18/19
 //             the high half written, 20/21/22 the low half written
+//   victims 24-27: the form pk_bisect.py isolated (a packed add whose destination is its second
+//             source with the halves crossed), its controls and a no-nop variant (inline asm)
 //   aggressors: 0 none, 1 MFMA f16, 2 LDS traffic, 3 victim-0 itself, 4 FP32 FMA, 5 FP64 FMA,
 //               6 DPP moves, 7 ds_bpermute, 8 v_permlane32_swap, 9 f32 transcendentals,
 //               10 f64 transcendentals (v_rcp_f64 / v_sqrt_f64)
@@ -263,6 +265,35 @@ __global__ __launch_bounds__(512) void victim(int iters, unsigned long long* bad
         y = rh * 0.25f + 0.5f;
       }
 #undef PK_SEQ
+      const bool mism = (__float_as_int(x) != __builtin_amdgcn_readfirstlane(__float_as_int(x))) |
+                        (__float_as_int(y) != __builtin_amdgcn_readfirstlane(__float_as_int(y)));
+      const unsigned long long d = mism ? 1ull : 0ull;
+      nb += (lane >= 48) ? (d << 32) : d;
+      nc += 64;
+    } else if (VICTIM >= 24 && VICTIM <= 27) {
+      // the instruction tools/ubench/pk_bisect.py isolated in victim 9: a packed add whose
+      // destination pair is its second source with the halves crossed (lo = a.lo + b.hi,
+      // hi = a.hi + b.lo, b = the destination); 25: the same op into a separate pair; 26: the
+      // destination as the second source without crossing; 27: as 24 with no s_nop before it
+      float x = 1.0f + 1e-3f * (float)(val(w, it, 0, 0) & 255), y = 1.0f - 1e-3f * (float)(val(w, it, 0, 1) & 255);
+      float rl = 0.0f, rh = 0.0f;
+#define PK_X(PRE, OP)                                                                                 \
+  asm volatile("v_mov_b32 v200, %2\n\tv_mov_b32 v201, %3\n\tv_mov_b32 v202, 0x3f400000\n\t"           \
+               "v_mov_b32 v203, 0x3fa00000\n\t" PRE OP "\n\ts_nop 7\n\t"                                \
+               "v_mov_b32 %0, v200\n\tv_mov_b32 %1, v201"                                              \
+               : "=v"(rl), "=v"(rh) : "v"(x), "v"(y) : "v200", "v201", "v202", "v203", "v204", "v205")
+#pragma unroll 2
+      for (int k = 0; k < 64; ++k) {
+        if (VICTIM == 24) PK_X("s_nop 7\n\t", "v_pk_add_f32 v[200:201], v[202:203], v[200:201] op_sel:[0,1] op_sel_hi:[1,0]");
+        else if (VICTIM == 25)
+          PK_X("s_nop 7\n\t", "v_pk_add_f32 v[204:205], v[202:203], v[200:201] op_sel:[0,1] op_sel_hi:[1,0]\n\t"
+                               "s_nop 7\n\tv_mov_b32 v200, v204\n\tv_mov_b32 v201, v205");
+        else if (VICTIM == 26) PK_X("s_nop 7\n\t", "v_pk_add_f32 v[200:201], v[202:203], v[200:201]");
+        else PK_X("", "v_pk_add_f32 v[200:201], v[202:203], v[200:201] op_sel:[0,1] op_sel_hi:[1,0]");
+        x = rl * 0.25f + 0.75f;
+        y = rh * 0.25f + 0.5f;
+      }
+#undef PK_X
       const bool mism = (__float_as_int(x) != __builtin_amdgcn_readfirstlane(__float_as_int(x))) |
                         (__float_as_int(y) != __builtin_amdgcn_readfirstlane(__float_as_int(y)));
       const unsigned long long d = mism ? 1ull : 0ull;
@@ -555,6 +586,10 @@ int main(int argc, char** argv) {
   else if (vk == 20) hipLaunchKernelGGL(victim<20>, vg, vb, 0, sv, iters, d, d + 1);
   else if (vk == 21) hipLaunchKernelGGL(victim<21>, vg, vb, 0, sv, iters, d, d + 1);
   else if (vk == 22) hipLaunchKernelGGL(victim<22>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 24) hipLaunchKernelGGL(victim<24>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 25) hipLaunchKernelGGL(victim<25>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 26) hipLaunchKernelGGL(victim<26>, vg, vb, 0, sv, iters, d, d + 1);
+  else if (vk == 27) hipLaunchKernelGGL(victim<27>, vg, vb, 0, sv, iters, d, d + 1);
   else hipLaunchKernelGGL(victim<2>, vg, vb, 0, sv, iters, d, d + 1);
   CK(hipGetLastError());
   CK(hipEventRecord(done, sv));

@@ -79,7 +79,17 @@ def expand(line):
         return [lo, hi]
     if d_hi not in lo_src:
         return [hi, lo]
-    return None  # both halves read the other's destination: left packed
+    # each half reads the other's destination (a half-swapped source, e.g. op_sel:[0,1] on the
+    # destination pair): swap the pair's halves first, then both halves read their own register
+    if name != "v_pk_mov_b32" and d_hi in lo_src and d_lo in hi_src:
+        op = lo.split()[0]
+        lo_s = [d_lo if x == d_hi else x for x in lo_src]
+        hi_s = [d_hi if x == d_lo else x for x in hi_src]
+        if d_hi in lo_s or d_lo in hi_s:
+            return None
+        return ["v_swap_b32 %s, %s" % (d_lo, d_hi), "%s %s, %s" % (op, d_lo, ", ".join(lo_s)),
+                "%s %s, %s" % (op, d_hi, ", ".join(hi_s))]
+    return None  # left packed
 
 
 def packed_lines(asm):
@@ -139,6 +149,22 @@ def main():
     none = run(outdir, lines, idx, set(fixed), "none_packed", iters)
     if full == 0:
         print("no disagreement with every instruction packed: nothing to bisect")
+        return
+    if none > 0:
+        print("the disagreement stays with every expandable instruction unpacked")
+    # one packed instruction at a time, every other one unpacked (a single-instruction cause shows
+    # here directly), and each instruction alone unpacked in the packed code
+    singles = [n for n in range(len(idx)) if n not in fixed]
+    hits = []
+    for n in singles:
+        if run(outdir, lines, idx, {n} | set(fixed), "only_%02d" % n, iters) > 0:
+            hits.append(n)
+    print("instructions that reproduce alone (every other one unpacked): %s" % hits)
+    for n in hits:
+        print("  %2d %s" % (n, lines[idx[n]].strip()))
+        run(outdir, lines, idx, {n} | set(fixed), "only_%02d_alone" % n, iters, aggr=0)
+        run(outdir, lines, idx, allset - {n}, "all_but_%02d" % n, iters)
+    if hits:
         return
     # delta debugging over the kept set (ddmin, complements first)
     keep = sorted(allset - set(fixed))
