@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase breakdown of the persistent kernel (diagnostic stamp build), rounds 11 and 12.
 Stamps: 0 round start, 1 partial published, 2 leader: sweep done / others: pose received,
-3 leader: solve done."""
+3 leader: solve done; and the leader's sweep passes (issue, return) of thread 0."""
 import argparse
 import ctypes
 import os
@@ -26,10 +26,14 @@ def main():
     assert info["mode"] == "persistent", info
     b.set_data(p["xyz"], p["uv"])
     b.set_poses(p["T_init"][None])
-    for _ in range(3):
-        b.solve(threshold=3000.0, max_rounds=50, conv_eps=-1.0)
-    nb = info["n_blocks"]
     L = picp_amd.lib()
+    L.picp_debug_sweepstamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    sw = np.zeros((2, 64), np.uint64)
+    for _ in range(3):
+        assert L.picp_debug_sweepstamps(sw.ctypes.data, sw.size) == 0  # read = clear
+        b.solve(threshold=3000.0, max_rounds=50, conv_eps=-1.0)
+    assert L.picp_debug_sweepstamps(sw.ctypes.data, sw.size) == 0
+    nb = info["n_blocks"]
     L.picp_debug_pstamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     buf = np.zeros((2, 256, 8), np.uint64)
     assert L.picp_debug_pstamps(buf.ctypes.data, buf.size) == 0
@@ -42,6 +46,17 @@ def main():
         others = rel[1:]
         for k, nm in enumerate(["start", "published", "pose_received"]):
             print("  others %-14s median %6d  min %6d  max %6d" % (nm, np.median(others[:, k]), others[:, k].min(), others[:, k].max()))
+        # the leader's sweep passes (thread 0): issue -> loads returned, ns from the round start
+        p = sw[r].astype(np.int64)
+        n = int(np.count_nonzero(p)) // 2
+        passes = [((p[2 * i] - t0) * 10, (p[2 * i + 1] - t0) * 10) for i in range(n)]
+        last_pub = int(others[:, 1].max())
+        print("  leader sweep passes (issue..return ns): %s" % "  ".join("%d..%d" % x for x in passes))
+        if passes:
+            dur = [b - a for a, b in passes]
+            after = [x for x in passes if x[0] >= last_pub]
+            print("  pass duration median %d ns (min %d max %d); %d passes, %d issued after the last publish (%d)" %
+                  (np.median(dur), min(dur), max(dur), n, len(after), last_pub))
     nxt = (buf[1, :nb, 0].astype(np.int64).min() - buf[0, :nb, 0].astype(np.int64).min()) * 10
     print("round period (first start r11 -> first start r12): %d ns" % nxt)
 
