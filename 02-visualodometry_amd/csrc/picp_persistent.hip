@@ -35,13 +35,6 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #ifndef PICP_PWIDE
 #define PICP_PWIDE 0
 #endif
-// -DPICP_SWEEP_WAIT=M (A/B, 10-ns ticks; 0 off): each leader wave sleeps before its first sweep
-// pass until the time, after its own publish, at which the previous round's completing pass
-// began, less M.  The sweep stamps (tools/pstamps.py) show the first pass of a round issued
-// before most partials land, so the next pass reloads nearly all of them (passes 0.6-0.8 us).
-#ifndef PICP_SWEEP_WAIT
-#define PICP_SWEEP_WAIT 0
-#endif
 // Followers' pose wait: two polls in flight this many s_sleep units (64 clocks) apart (0: one)
 #ifndef PICP_POSE_STAGGER
 #define PICP_POSE_STAGGER 8
@@ -177,7 +170,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
 
   float chi_prev = FLT_MAX;  // the leader's loop state besides the pose (exec/icp_test.cpp:89)
   unsigned long long pose_sink = 0, pa = 0, pb = 0, pc = 0;  // the follower's pose polls (PICP_POSE_STAGGER)
-  [[maybe_unused]] unsigned long long sweep_wait = 0;  // the leader wave's sleep before its first pass (PICP_SWEEP_WAIT)
   for (unsigned epoch = 1; !s_done; ++epoch) {
     // every wait of this round is bounded from the round's start (a whole solve may take far
     // longer than timeout_ticks at large max_rounds; one round never does)
@@ -252,22 +244,9 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         if (g + NG * i < nblk) pending |= 1u << i;
       }
       [[maybe_unused]] int npass = 0;  // sweep passes (diagnostic stamps)
-#if PICP_SWEEP_WAIT
-      // the first pass no earlier than the previous round's completing pass less the margin: an
-      // early pass finds most partials not yet landed and the next one reloads them all
-      const unsigned long long t_sw = __builtin_amdgcn_s_memrealtime();
-      if (sweep_wait > 0) {
-        const unsigned long long until = t_sw + sweep_wait;
-        while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(1);
-      }
-      unsigned long long t_pass = t_sw;
-#endif
       for (;;) {
         const unsigned want = pending;  // issue every pending load before checking any tag
         SWSTAMP(2 * npass);
-#if PICP_SWEEP_WAIT
-        t_pass = __builtin_amdgcn_s_memrealtime();
-#endif
 #pragma unroll
         for (int i = 0; i < MAXG; ++i)
           if (want & (1u << i))
@@ -286,13 +265,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         }
         PICP_POLL_PAUSE();
       }
-#if PICP_SWEEP_WAIT
-      {  // next round: wait until this round's completing pass began, less the margin (<= 5 us)
-        const unsigned long long seen = t_pass - t_sw;
-        sweep_wait = (seen > PICP_SWEEP_WAIT) ? seen - PICP_SWEEP_WAIT : 0ull;
-        sweep_wait = sweep_wait < 500ull ? sweep_wait : 500ull;
-      }
-#endif
       double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
       for (int i = 0; i < MAXG; ++i)
