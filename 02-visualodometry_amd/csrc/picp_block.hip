@@ -254,7 +254,6 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     const VoT vo, int vo_t) {
   constexpr bool VOA = std::is_same<VoT, VoAppend>::value;  // ... and the append after the rounds
   constexpr bool VOG = std::is_same<VoT, VoArgs>::value || VOA;  // the VO step's gather fused in
-  PICP_KFENCE_IN();
   BSTAMP_PLACE();
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   // wave sums, term-major: the lane combining term e reads its BS/64 wave sums as 16-B loads
@@ -538,7 +537,6 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
   if (h == 0 && tid < 32)
     reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
   if constexpr (VOA) vo_append_body<BS>(vo, vo_t, vo.seg0 + p, &s_st, n);  // s_st: after the last barrier
-  PICP_KFENCE_OUT();
 }
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part (BS 512)

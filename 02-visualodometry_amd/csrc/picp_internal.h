@@ -92,23 +92,6 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 #define PICP_FINISH_WAVE 0
 #endif
 
-// Diagnostic build only (-DPICP_KFENCE): explicit agent-scope acquire at the start and release at
-// the end of the VO path's kernels, to test whether kernel-boundary visibility is what differs
-// between schedules.
-#if defined(PICP_KFENCE_SYS)  // system scope: also writes back / invalidates the XCD's L2
-#define PICP_KFENCE_IN() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "")
-#define PICP_KFENCE_OUT() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "")
-#elif defined(PICP_KFENCE)
-#define PICP_KFENCE_IN() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
-#define PICP_KFENCE_OUT() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
-#else
-#define PICP_KFENCE_IN() \
-  do {                   \
-  } while (0)
-#define PICP_KFENCE_OUT() \
-  do {                    \
-  } while (0)
-#endif
 
 struct MatchProblem {
   int64_t q_off, nq, r_off, nr;

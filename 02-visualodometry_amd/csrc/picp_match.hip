@@ -375,7 +375,6 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
     float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
     int xcd_map) {
-  PICP_KFENCE_IN();
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
@@ -842,7 +841,6 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
                 accepted);  // :100-103
   }
-  PICP_KFENCE_OUT();
 }
 
 extern "C" int picp_match_prep_kch(int dim) { return dim <= 16 ? 1 : 2; }

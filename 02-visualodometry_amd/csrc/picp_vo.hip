@@ -42,14 +42,12 @@ using namespace picp;
 #endif
 
 __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int t) {
-  PICP_KFENCE_IN();
   const int s = a.seg0 + (int)blockIdx.x;
   const VoSegment G = a.segs[s];
   const int64_t base = (int64_t)s * a.cap_c;
   __shared__ int s_cnt[VO_WAVES];
   if (t >= G.steps) {  // segment finished: an empty problem (its result is never read)
     if (threadIdx.x == 0) a.probs[s] = PicpProblem{base, 0, 0, 1, 0};
-    PICP_KFENCE_OUT();
     return;
   }
   const int64_t nf = G.f0 + t + 1;
@@ -109,14 +107,11 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
     cnt += tot;
   }
   if (threadIdx.x == 0) a.probs[s] = PicpProblem{base, (int32_t)cnt, 0, 1, 0};
-  PICP_KFENCE_OUT();
 }
 
 __global__ __launch_bounds__(VOA_BLOCK) void vo_append_kernel(const VoArgs a, int t) {
-  PICP_KFENCE_IN();
   const int s = a.seg0 + (int)blockIdx.x;
   vo_append_body<VOA_BLOCK>(a, t, s, a.st_out + s, (t < 0) ? 0 : a.probs[s].n);
-  PICP_KFENCE_OUT();
 }
 
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t) {
