@@ -553,23 +553,12 @@ static int s4_bs() {
 }
 extern "C" int picp_block_threads(int split) { return (split == 4) ? s4_bs() : PICP_BBLOCK; }
 
-// PICP_BLOCK_DUAL=1 (A/B): one block per problem, TWO blocks per CU -- the 128-VGPR kernel (MINW 4,
-// at most four register items per lane) and half the LDS stage, the rest streamed -- so that one
-// problem's round tail runs under the other's linearize, as split 4 does without its exchange.
-static bool dual1() {
-  static const bool d = [] {
-    const char* e = getenv("PICP_BLOCK_DUAL");
-    return e && atoi(e) == 1;
-  }();
-  return d;
-}
-
 // dynamic LDS of a launch: the part of a problem (or of its 1/split share) past the
 // register-resident npt x BS items, capped by the stage
-static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out, bool dual = false) {
+static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out) {
   const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
   const int bs = picp_block_threads(split);
-  const int lds_cap = (split == 4 || dual) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
+  const int lds_cap = (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
   const int lds_items = (per_block > npt * bs) ? min(per_block - npt * bs, lds_cap) : 0;
   if (lds_items_out) *lds_items_out = lds_items;
   return (size_t)5 * lds_items * sizeof(float);
@@ -588,7 +577,7 @@ static const void* block_kernel_nbw(int var) {
 template <int N>
 static const void* block_kernel_n(int var, int bs, int split) {
   if (bs == 256) return block_kernel_nbw<N, 256, 2>(var);
-  if (split == 4 || (split == 1 && dual1())) {
+  if (split == 4) {
     if constexpr (N <= 4) return block_kernel_nbw<N, 512, 4>(var);  // <= 128 VGPRs: NPT <= 4
     return nullptr;
   }
@@ -606,9 +595,7 @@ static const void* block_kernel_ptr(int npt, int var, int bs, int split) {
 }
 
 // Register items per lane the split-4 512-thread layout allows (its 128-VGPR budget); 8 otherwise.
-extern "C" int picp_block_npt_cap(int split) {
-  return ((split == 4 && s4_bs() == 512) || (split == 1 && dual1())) ? 4 : 8;
-}
+extern "C" int picp_block_npt_cap(int split) { return (split == 4 && s4_bs() == 512) ? 4 : 8; }
 
 // Blocks of the variants a launch with these arguments may use that one CU holds at once (the
 // hardware limit from registers, LDS and waves; other work on the device is not counted; the
@@ -618,7 +605,7 @@ extern "C" int picp_block_npt_cap(int split) {
 extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu) {
   if (!blocks_per_cu || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
   const int bs = picp_block_threads(split);
-  const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr, split == 1 && dual1());
+  const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr);
   int best = -1;
   for (int keep = 0; keep < 2; ++keep) {
     const void* fn = block_kernel_ptr(npt, picp_variant(K, keep), bs, split);
@@ -657,7 +644,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
   const void* fn = block_kernel_ptr(npt, var, bs, split);
   if (!fn) return hipErrorInvalidValue;
   int lds_items = 0;
-  const size_t lds_bytes = block_lds_bytes(npt, split, max_n, &lds_items, split == 1 && dual1());
+  const size_t lds_bytes = block_lds_bytes(npt, split, max_n, &lds_items);
   if (lds_bytes > 65536) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   NoVo novo{};
   int zero = 0;

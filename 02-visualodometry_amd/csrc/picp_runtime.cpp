@@ -406,12 +406,6 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
         split = (split == 4) ? 2 : 1;
       }
       b->split = split;
-      if (split == 1) {  // register items per lane under the layout's VGPR budget (PICP_BLOCK_DUAL)
-        int cap = std::min(picp_block_max_items() / 512, picp_block_npt_cap(1));
-        if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
-        bnpt = 1;
-        while (bnpt < cap && (int64_t)bnpt * 512 < max_n) bnpt *= 2;
-      }
       if (split > 1) {  // register items per lane for a part
         const int64_t part = round_up((max_n + split - 1) / split, 4);
         const int bs = picp_block_threads(split);
