@@ -23,30 +23,18 @@
 // deadline, refreshed each round (error word set, the problem stops, the host reports it and
 // re-runs the solve in graph mode).  The host launches a split grid only when the occupancy query
 // below says every block is resident at once.
-// split = 4 uses 256-thread blocks (BS = 256), two per CU from DIFFERENT problems: while one
-// problem's parts exchange and solve (the CU idle in split = 2), the other's compute; the
-// hardware issues the older block first, so the two settle into alternating phases.
+// split = 4 runs two 512-thread blocks per CU from DIFFERENT problems (<= 128 VGPRs each): while
+// one problem's parts exchange and solve (the CU idle in split = 2), the other's compute.
 #include <type_traits>
 
 #include "picp_vo_device.h"
 
 using namespace picp;
 
-#define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs (split 1, 2); 256 for split 4
+#define PICP_BBLOCK 512  // 8 waves: 2 per SIMD at <= 256 VGPRs (split 1, 2); 4 per SIMD for split 4
 #define PICP_BLDS_ITEMS 7680  // items staged in LDS: 5 x 4 B x 7680 = 150 KB of the 160 KB per CU
 // partner polls run back to back: an s_sleep 1 between polls measured C4 1704-1711 us vs
 // 1700-1706 us without it, 4 of 4 interleaved reps (profiles/r02/e4/ab_bspin.log).
-// -DPICP_BPOLL_SLEEP restores the pause for A/B runs.
-#ifdef PICP_BPOLL_SLEEP
-#define PICP_BPOLL_PAUSE() __builtin_amdgcn_s_sleep(1)
-#else
-#define PICP_BPOLL_PAUSE() ((void)0)
-#endif
-// The split exchange's poll: every partner's granules loaded before any is checked (default), or
-// partner by partner (-DPICP_XG_BATCH=0, round 3's form; A/B).
-#ifndef PICP_XG_BATCH
-#define PICP_XG_BATCH 1
-#endif
 #define PICP_XG 64            // exchange granules per block per round: 32 hi + 32 lo
 
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
@@ -91,9 +79,6 @@ extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words
 // clamp did.  Needs n <= NPT*BS + lds_items and frames of <= VOG_CHUNKS*BS observations (the
 // host's check).  Writes a.probs[s] (the append reads n) and returns n.
 struct NoVo {};
-// VoT = VoAppend: the step's append (picp_vo_device.h vo_append_body) runs in the same block after
-// the rounds, on the final state in LDS, instead of in vo_append_kernel
-struct VoAppend : VoArgs {};
 #define VOG_CHUNKS 8  // observation chunks of BS held in registers: 4096 at BS 512
 #define VOG_SLICE 256  // items per pass of the register transfer
 template <int NPT, int BS>
@@ -227,16 +212,9 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
 #ifndef PICP_BPRIO
 #define PICP_BPRIO 1
 #endif
-// -DPICP_VOPRIO (A/B): in the VO step's form the linearize runs at priority 2 as well, so the
-// matcher waves that share the CU (the split world match's early part, the frame->next chunks,
-// priority 0) take only the issue slots the step chain leaves.
 #if PICP_BPRIO
 #define BPRIO_TAIL() __builtin_amdgcn_s_setprio(3)
-#ifdef PICP_VOPRIO
-#define BPRIO_LIN() (VOG ? __builtin_amdgcn_s_setprio(2) : __builtin_amdgcn_s_setprio(0))
-#else
 #define BPRIO_LIN() __builtin_amdgcn_s_setprio(0)
-#endif
 #else
 #define BPRIO_TAIL() ((void)0)
 #define BPRIO_LIN() ((void)0)
@@ -252,8 +230,7 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
     PicpState* __restrict__ st_out, int lds_items, int split, int n_problems,
     unsigned long long* xg, unsigned int* err, unsigned int* tagbase, unsigned long long timeout_ticks,
     const VoT vo, int vo_t) {
-  constexpr bool VOA = std::is_same<VoT, VoAppend>::value;  // ... and the append after the rounds
-  constexpr bool VOG = std::is_same<VoT, VoArgs>::value || VOA;  // the VO step's gather fused in
+  constexpr bool VOG = std::is_same<VoT, VoArgs>::value;  // the VO step's gather fused in
   BSTAMP_PLACE();
   extern __shared__ float s_lds[];  // [5][lds_items]: the problem's items past the registers
   // wave sums, term-major: the lane combining term e reads its BS/64 wave sums as 16-B loads
@@ -455,10 +432,9 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
         }
         part_t[h & 3] = (double)hi + (double)lo;
         for (;;) {
-#if PICP_XG_BATCH
           // every partner's two granules loaded before any tag is checked (the partners are a
           // block-uniform set, so the loads issue back to back): one round trip per poll.  Checking
-          // each partner right after its loads (PICP_XG_BATCH=0) waited one round trip per
+          // each partner right after its loads (round 3's form) waited one round trip per
           // partner, three per poll at split 4.
           unsigned long long gh[4], gl[4];
 #pragma unroll
@@ -477,27 +453,12 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
               pending &= ~(1u << q);
             }
           }
-#else
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (!(pending & (1u << q))) continue;
-            const bgu64_t* theirs = xgg + (slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * PICP_XG;
-            const unsigned long long gh = __hip_atomic_load(theirs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long gl =
-                __hip_atomic_load(theirs + PICP_NPART + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(gh >> 32) == tag && (unsigned)(gl >> 32) == tag) {
-              part_t[q] = (double)__uint_as_float((unsigned)gh) + (double)__uint_as_float((unsigned)gl);
-              pending &= ~(1u << q);
-            }
-          }
-#endif
           if (!pending) break;
           if (__builtin_amdgcn_s_memrealtime() > deadline) {
             __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_tmo = 1;
             break;
           }
-          PICP_BPOLL_PAUSE();
         }
         t = part_t[0];
 #pragma unroll
@@ -536,22 +497,14 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
   if (split > 1 && tid == 0) tagbase[blockIdx.x] = tbase + (unsigned)last_round;
   if (h == 0 && tid < 32)
     reinterpret_cast<int32_t*>(&st_out[p])[tid] = reinterpret_cast<const int32_t*>(&s_st)[tid];
-  if constexpr (VOA) vo_append_body<BS>(vo, vo_t, vo.seg0 + p, &s_st, n);  // s_st: after the last barrier
 }
 
 extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // register-resident part (BS 512)
 
-// Threads per block of a split layout: 512 for split 1 and 2 (one block per CU); split 4 runs two
-// blocks per CU, either 256-thread blocks (one wave per SIMD each, <= 256 VGPRs) or 512-thread
-// blocks (two waves per SIMD each, <= 128 VGPRs: MINW 4).
-static int s4_bs() {
-  static const int bs = [] {
-    const char* e = getenv("PICP_BLOCK_S4BS");
-    return (e && atoi(e) == 256) ? 256 : 512;
-  }();
-  return bs;
-}
-extern "C" int picp_block_threads(int split) { return (split == 4) ? s4_bs() : PICP_BBLOCK; }
+// Threads per block: 512 for every split; split 4 runs two blocks per CU (two waves per SIMD each,
+// <= 128 VGPRs: MINW 4).  256-thread split-4 parts (round 1) measured 5-7 % slower
+// (profiles/r01/c4_split4_ab.log, profiles/r04/c4_128/).
+extern "C" int picp_block_threads(int split) { return (void)split, PICP_BBLOCK; }
 
 // dynamic LDS of a launch: the part of a problem (or of its 1/split share) past the
 // register-resident npt x BS items, capped by the stage
@@ -564,38 +517,37 @@ static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out)
   return (size_t)5 * lds_items * sizeof(float);
 }
 
-// the kernel of a launch: (threads, waves per SIMD) = (512, 2), (256, 2) or split 4's (512, 4)
-template <int N, int B, int W>
-static const void* block_kernel_nbw(int var) {
+// the kernel of a launch: waves per SIMD 2 (split 1, 2) or split 4's 4
+template <int N, int W>
+static const void* block_kernel_nw(int var) {
   switch (var) {
-    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, B, NoVo, W>;
-    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, B, NoVo, W>;
-    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, B, NoVo, W>;
+    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, PICP_BBLOCK, NoVo, W>;
+    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, PICP_BBLOCK, NoVo, W>;
+    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, PICP_BBLOCK, NoVo, W>;
   }
 }
 
 template <int N>
-static const void* block_kernel_n(int var, int bs, int split) {
-  if (bs == 256) return block_kernel_nbw<N, 256, 2>(var);
+static const void* block_kernel_n(int var, int split) {
   if (split == 4) {
-    if constexpr (N <= 4) return block_kernel_nbw<N, 512, 4>(var);  // <= 128 VGPRs: NPT <= 4
+    if constexpr (N <= 4) return block_kernel_nw<N, 4>(var);  // <= 128 VGPRs: NPT <= 4
     return nullptr;
   }
-  return block_kernel_nbw<N, 512, 2>(var);
+  return block_kernel_nw<N, 2>(var);
 }
 
-static const void* block_kernel_ptr(int npt, int var, int bs, int split) {
+static const void* block_kernel_ptr(int npt, int var, int split) {
   switch (npt) {
-    case 1: return block_kernel_n<1>(var, bs, split);
-    case 2: return block_kernel_n<2>(var, bs, split);
-    case 4: return block_kernel_n<4>(var, bs, split);
-    case 8: return block_kernel_n<8>(var, bs, split);
+    case 1: return block_kernel_n<1>(var, split);
+    case 2: return block_kernel_n<2>(var, split);
+    case 4: return block_kernel_n<4>(var, split);
+    case 8: return block_kernel_n<8>(var, split);
     default: return nullptr;
   }
 }
 
-// Register items per lane the split-4 512-thread layout allows (its 128-VGPR budget); 8 otherwise.
-extern "C" int picp_block_npt_cap(int split) { return (split == 4 && s4_bs() == 512) ? 4 : 8; }
+// Register items per lane the split-4 layout allows (its 128-VGPR budget); 8 otherwise.
+extern "C" int picp_block_npt_cap(int split) { return (split == 4) ? 4 : 8; }
 
 // Blocks of the variants a launch with these arguments may use that one CU holds at once (the
 // hardware limit from registers, LDS and waves; other work on the device is not counted; the
@@ -608,7 +560,7 @@ extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const 
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr);
   int best = -1;
   for (int keep = 0; keep < 2; ++keep) {
-    const void* fn = block_kernel_ptr(npt, picp_variant(K, keep), bs, split);
+    const void* fn = block_kernel_ptr(npt, picp_variant(K, keep), split);
     if (!fn) return hipErrorInvalidValue;
     if (lds_bytes > 65536) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
@@ -625,8 +577,8 @@ extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const 
 
 // max_n: the largest problem of the launch (sizes the LDS stage: max_n/split - npt*BS items,
 // capped).  split = 1: grid = n_problems blocks of 512.  split = 2: grid = round_up(2 n_problems,
-// 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of
-// picp_block_threads(4), two per CU; all co-resident (the caller checks the grid against the
+// 16) blocks of 512, one per CU; split = 4: grid = round_up(4 n_problems, 32) blocks of 512, two
+// per CU; all co-resident (the caller checks the grid against the
 // CUs), xg = 2 * grid * 64 u64 granules, tagbase = grid u32 tag bases (both zeroed once per
 // layout), err the error word.
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
@@ -641,7 +593,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
   const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
   const int var = picp_variant(args->K, args->keep_outliers);
   const int bs = picp_block_threads(split);
-  const void* fn = block_kernel_ptr(npt, var, bs, split);
+  const void* fn = block_kernel_ptr(npt, var, split);
   if (!fn) return hipErrorInvalidValue;
   int lds_items = 0;
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, &lds_items);
@@ -666,29 +618,22 @@ extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs) {
          (npt == 1 || npt == 2 || npt == 4 || npt == 8);
 }
 
-// append = 1: the step's append runs in the same kernel after the rounds (VoAppend); the caller
-// orders the launch after everything the append reads (the step's frame->next match).
 extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
-                                           const PicpArgs* args, int64_t max_obs, int append) {
+                                           const PicpArgs* args, int64_t max_obs) {
   if (!a || !args || a->n_seg <= 0 || !picp_vo_block_fusable(npt, max_obs)) return hipErrorInvalidValue;
   int lds_items = 0;
   const size_t lds_bytes = block_lds_bytes(npt, 1, (int)max_obs, &lds_items);
   const int var = picp_variant(args->K, args->keep_outliers);
-  VoAppend va;
-  static_cast<VoArgs&>(va) = *a;
-#define PICP_LAUNCH_VB4(N, P, VT, VV)                                                                       \
+#define PICP_LAUNCH_VB3(N, P)                                                                              \
   {                                                                                                        \
     if (lds_bytes > 65536)                                                                                 \
-      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, PICP_BBLOCK, VT>,                           \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>,                       \
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);                     \
-    hipLaunchKernelGGL((picp_block_kernel<N, P, PICP_BBLOCK, VT>), dim3(a->n_seg), dim3(PICP_BBLOCK),      \
+    hipLaunchKernelGGL((picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>), dim3(a->n_seg), dim3(PICP_BBLOCK),  \
                        lds_bytes, stream, a->X, a->Y, a->Z, a->U, a->V, *args, a->probs + a->seg0,          \
                        a->st_in + a->seg0, (PicpState*)a->st_out + a->seg0, lds_items, 1, a->n_seg,         \
-                       nullptr, nullptr, nullptr, 0ull, VV, t);                                            \
+                       nullptr, nullptr, nullptr, 0ull, *a, t);                                            \
   }
-#define PICP_LAUNCH_VB3(N, P)                 \
-  if (append) PICP_LAUNCH_VB4(N, P, VoAppend, va) \
-  else PICP_LAUNCH_VB4(N, P, VoArgs, *a)
 #define PICP_LAUNCH_VB(N)                                                        \
   if (var == PICP_V_PINHOLE) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE)                   \
   else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE_KEEP)    \
@@ -702,6 +647,5 @@ extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, 
   }
 #undef PICP_LAUNCH_VB
 #undef PICP_LAUNCH_VB3
-#undef PICP_LAUNCH_VB4
   return hipGetLastError();
 }

@@ -95,10 +95,6 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 
 struct MatchProblem {
   int64_t q_off, nq, r_off, nr;
-  // merge = 1: the references before r_off were matched into the output rows by an earlier launch
-  // (the VO sequence's split world match): this launch's top-2 over [r_off, r_off + nr) is merged
-  // into those rows, its indices offset by idx_base (relative to the earlier launch's r_off)
-  int64_t idx_base, merge;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -160,12 +156,6 @@ struct VoArgs {     // by value; every pointer is device memory
   PicpState* st_in;
   const PicpState* st_out;
   MatchProblem* wprobs;      // next step's world-match problem of each segment
-  // the split world match (picp_vo_runtime.cpp PICP_VO_SPLIT): next step's late part (the map
-  // points the append just added, merged into the early part's rows) and the step after next's
-  // early part (the map as it is now), the latter double-buffered by step parity: [2][n_seg_all]
-  MatchProblem* lprobs;
-  MatchProblem* eprobs;
-  int32_t n_seg_all;
   float* poses;              // 16 per slot, camera-in-world, column-major
   VoStep* steps;
   int2* pairs;               // append scratch: segment s at s * cap_c

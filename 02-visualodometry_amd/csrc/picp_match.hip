@@ -47,28 +47,11 @@ __device__ inline void match_update(float d, int32_t j, float& best, float& seco
 
 // One query's outputs: best index (relative to the problem's r_off), best and second distance,
 // and the reference's accept test (src/my_utilities.h:100-103: best < DISTANCE_THRESHOLD and
-// best/second < RATIO_THRESHOLD).  With P.merge the row already holds an earlier launch's top-2
-// over the references BEFORE this problem's (indices relative to that launch's r_off): the two
-// are merged as the reference's in-order scan would continue over this problem's references --
-// best = the smaller (a tie keeps the earlier, lower index), second = the second smallest of the
-// union (min of the larger best and the smaller side's second) -- and this launch's indices are
-// offset by P.idx_base.  Neither distance is ever NaN (match_update maps NaN to +inf).
+// best/second < RATIO_THRESHOLD).  Neither distance is ever NaN (match_update maps NaN to +inf).
 __device__ __forceinline__ void match_store(const MatchProblem& P, int64_t o, int32_t bi, float best, float second,
                                             float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
                                             float* second_dist, int32_t* accepted) {
-  if (P.merge) {
-    const float pb = best_dist[o], ps = second_dist[o];
-    const int32_t pi = best_idx[o];
-    const int32_t gi = (bi < 0) ? -1 : (int32_t)(bi + P.idx_base);
-    if (pb <= best) {
-      second = (ps < best) ? ps : best;
-      best = pb;
-      bi = pi;
-    } else {
-      second = (pb < second) ? pb : second;
-      bi = gi;
-    }
-  }
+  (void)P;
   best_idx[o] = bi;
   best_dist[o] = best;
   second_dist[o] = second;

@@ -42,14 +42,6 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
                                         unsigned int* tagbase, unsigned long long timeout_ticks);
-extern "C" hipError_t picp_launch_pair(hipStream_t stream, int n_problems, int npt, const float* X, const float* Y,
-                                       const float* Z, const float* U, const float* V, const PicpArgs* args,
-                                       const PicpState* st_in, PicpState* st_out, int max_n, int split,
-                                       unsigned long long* xg, unsigned int* err, unsigned int* tagbase,
-                                       unsigned long long timeout_ticks);
-extern "C" hipError_t picp_pair_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu);
-extern "C" int picp_pair_grid(int n_problems, int split);
-extern "C" int picp_pair_npt_cap(void);
 extern "C" int picp_block_max_items(void);
 extern "C" int picp_block_threads(int split);
 extern "C" int picp_block_npt_cap(int split);
@@ -197,7 +189,6 @@ struct picp_batch {
   int64_t stride_u = 0;
   int num_cu = 256;            // compute units of the device
   int split = 1;               // block mode: blocks per problem (1, or 2 when 2*np fits the chip)
-  int pair = 0;                // block mode: two problems per block, rounds interleaved (picp_pair.hip)
   int mode = PICP_MODE_GRAPH;  // PICP_MODE_GRAPH (launch per round) / PICP_MODE_PERSISTENT
   int npt = 1;                 // persistent: correspondences per lane held in registers
   unsigned char* sync = nullptr;   // persistent: [err 16 B | pose granules | partial granules | tag bases]
@@ -227,19 +218,13 @@ struct picp_batch {
 // persistent launches and split block launches hand off through granules and report a timed-out
 // wait in the error word at the head of b->sync
 static bool uses_err_word(const picp_batch* b) {
-  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && (b->split > 1 || b->pair));
+  return b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1);
 }
 
-// exchange granules / tag bases of a split block layout: (grid, granule sets per block)
-static void xg_layout(const picp_batch* b, int64_t* grid, int64_t* sets) {
+// exchange granules / tag bases of a split block layout: the grid (one granule set per block)
+static int64_t xg_grid(const picp_batch* b) {
   const int64_t ss = std::max(b->split, 1);
-  if (b->pair) {
-    *grid = picp_pair_grid((int)b->np, (int)ss);
-    *sets = 2;
-  } else {
-    *grid = ((ss * b->np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
-    *sets = 1;
-  }
+  return ((ss * b->np + 8 * ss - 1) / (8 * ss)) * (8 * ss);
 }
 
 static void drop_graph(picp_batch* b) {
@@ -379,7 +364,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
       // times the problems still fit two per CU and a part keeps >= 2048 correspondences (the C4
       // per-rank shape at N = 8, 128 frames x 10k): one block's round tail (at issue priority 3)
       // runs under the other's linearize; 22.0-22.4M vs 21.2-21.4M it/s for split 2
-      // (profiles/r04/p1/).  256-thread parts (PICP_BLOCK_S4BS=256, round 1) were 5 % slower.
+      // (profiles/r04/p1/).  256-thread parts (round 1) were 5 % slower.
       if (grid_of(4) <= 2 * b->num_cu && max_n >= 8192 && picp_block_threads(4) == 512) split = 4;
       if (b->no_handoff) split = 1;
       if (const char* e = getenv("PICP_BLOCK_SPLIT")) {
@@ -415,53 +400,11 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
         while (bnpt < cap && (int64_t)bnpt * bs < part) bnpt *= 2;
       }
       b->npt = bnpt;
-      // pair mode (picp_pair.hip): two problems per block, one problem's serial round tail under
-      // the other's linearize (uniform batches).  The widest split whose grid is one block per
-      // CU; more pairs than CUs take split 1, which has no cross-block waits.
-      // PICP_BLOCK_PAIR=0|1 forces it off / on.
-      b->pair = 0;
-      {
-        int want = 0;
-        if (const char* e = getenv("PICP_BLOCK_PAIR")) want = atoi(e) != 0;
-        if (want && b->uniform && np >= 2 && !b->no_handoff) {
-          int ps = 1;
-          for (int S : {4, 2}) {
-            if (picp_pair_grid(np, S) <= b->num_cu && max_n >= 1024 * S) {
-              ps = S;
-              break;
-            }
-          }
-          if (const char* e = getenv("PICP_BLOCK_SPLIT")) {
-            const int v = atoi(e);
-            if (v == 1 || ((v == 2 || v == 4) && picp_pair_grid(np, v) <= b->num_cu)) ps = v;
-          }
-          const int64_t part = round_up((max_n + ps - 1) / ps, 4);
-          int cap = picp_pair_npt_cap();
-          if (const char* e = getenv("PICP_BLOCK_NPT")) cap = std::max(1, std::min(cap, atoi(e)));
-          int pnpt2 = 1;
-          while (pnpt2 < cap && (int64_t)pnpt2 * 512 < part) pnpt2 *= 2;
-          bool ok = true;
-          if (ps > 1) {  // its blocks wait on each other: all of them resident at once
-            int occ = 0;
-            const int res = resident_per_cu(picp_pair_occupancy(pnpt2, ps, (int)max_n, b->K, &occ), occ) * b->num_cu;
-            ok = picp_pair_grid(np, ps) <= res;
-            if (ok) {
-              b->handoff_grid = picp_pair_grid(np, ps);
-              b->handoff_resident = res;
-            }
-          }
-          if (ok) {
-            b->pair = 1;
-            b->split = ps;
-            b->npt = pnpt2;
-          }
-        }
-      }
     }
   }
   // report the hand-off grid of the layout in use only (a candidate the occupancy check rejected
   // leaves no hand-off behind: picp_batch_residency then reads 0/0)
-  if (!(b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1))) {  // pair split 1: none
+  if (!(b->mode == PICP_MODE_PERSISTENT || (b->mode == PICP_MODE_BLOCK && b->split > 1))) {
     b->handoff_grid = 0;
     b->handoff_resident = 0;
   }
@@ -522,12 +465,11 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
     // persistent: error word | pose granules | partial granules (x2 parities);
     // split block: error word | exchange granules (x2 parities, 64 per block and problem held)
     // | tag bases
-    int64_t sgrid = 0, sets = 1;
-    xg_layout(b, &sgrid, &sets);
+    const int64_t sgrid = xg_grid(b);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
                         ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
                                                (int64_t)np * 4, 256)
-                        : (size_t)round_up(16 + 2 * sgrid * sets * 64 * 8 + sgrid * sets * 4, 256);
+                        : (size_t)round_up(16 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
       b->sync = nullptr;
@@ -652,16 +594,12 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
     unsigned int* err = nullptr;
     unsigned long long* xg = nullptr;
     unsigned int* tagbase = nullptr;
-    if (b->split > 1 || b->pair) {  // tags continue from the per-slot tag bases: no memset per launch
-      int64_t sgrid = 0, sets = 1;
-      xg_layout(b, &sgrid, &sets);
+    if (b->split > 1) {  // tags continue from the per-slot tag bases: no memset per launch
+      const int64_t sgrid = xg_grid(b);
       err = reinterpret_cast<unsigned int*>(b->sync);
       xg = reinterpret_cast<unsigned long long*>(b->sync + 16);
-      tagbase = reinterpret_cast<unsigned int*>(xg + 2 * sgrid * sets * 64);
+      tagbase = reinterpret_cast<unsigned int*>(xg + 2 * sgrid * 64);
     }
-    if (b->pair)
-      return picp_launch_pair(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args, b->init_d,
-                              b->st_d[0], (int)b->max_n, b->split, xg, err, tagbase, b->timeout_ticks);
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
                              b->probs_d, b->init_d, b->st_d[0], (int)b->max_n, b->split, xg, err, tagbase,
                              b->timeout_ticks);

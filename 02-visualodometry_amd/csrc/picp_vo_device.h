@@ -1,6 +1,6 @@
 // picp_vo_device.h -- device pieces of the VO step shared by the VO kernels (picp_vo.hip) and the
-// PICP block kernel's fused VO form (picp_block.hip): pose algebra, the ordered block compaction
-// and the append (exec/icp_test.cpp:113-132, src/my_utilities.cpp:413-434, src/cam.cpp:94-140).
+// PICP block kernel's fused VO gather (picp_block.hip): pose algebra, the ordered block
+// compaction and the append (exec/icp_test.cpp:113-132, src/my_utilities.cpp:413-434, src/cam.cpp:94-140).
 #pragma once
 #include "picp_device.h"
 
@@ -65,8 +65,7 @@ __device__ __forceinline__ int vo_block_rank(bool flag, int* s_cnt, int* total) 
 // record the PICP result, select the curr->next pairs whose next point has no map match (pass 1,
 // pair order), triangulate them with (previous pose, new pose) and append (xyz, curr descriptor)
 // to the map (pass 2), then write the next step's world-match problem and PICP initial state.
-// st: the PICP result (the block kernel's final state in LDS when fused; a.st_out[s] otherwise);
-// n_corr: the PICP input size (a.probs[s].n otherwise).  Contains barriers: every thread calls.
+// st_res: the PICP result (a.st_out[s]); n_corr: the PICP input size (a.probs[s].n).  Contains barriers: every thread calls.
 template <int NT>
 __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, const PicpState* st_res, int n_corr) {
   constexpr int NW = NT / 64;
@@ -220,19 +219,6 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
       wp.nq = a.frame_off[f + 1] - wp.q_off;
     }
     a.wprobs[s] = wp;
-    // the split world match: step tn's = the early part [0, m_prev) (matched beside the previous
-    // step; the bootstrap has none) + the late part [m_prev, mn) merged into its rows; step tn + 1's
-    // early part is [0, mn)
-    const int64_t m_prev = s_base;
-    MatchProblem lp{wp.q_off, wp.nq, G.map_off + m_prev, mn - m_prev, m_prev, boot ? 0 : 1};
-    a.lprobs[s] = lp;
-    MatchProblem ep{0, 0, G.map_off, mn, 0, 0};
-    if (tn + 1 < G.steps) {
-      const int64_t f = G.f0 + tn + 2;
-      ep.q_off = a.frame_off[f];
-      ep.nq = a.frame_off[f + 1] - ep.q_off;
-    }
-    a.eprobs[(size_t)((tn + 1) & 1) * a.n_seg_all + s] = ep;
     // PICP initial state: world-in-camera = previous_pose.inverse() (:78)
     float Twc[16];
     vo_iso_inverse(sTn, Twc);

@@ -42,7 +42,7 @@ extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a,
 extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs);
 extern "C" int picp_build_packed_fp32(void);
 extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
-                                           const PicpArgs* args, int64_t max_obs, int append);
+                                           const PicpArgs* args, int64_t max_obs);
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t);
 
 static_assert(sizeof(picp_vo_step) == sizeof(VoStep), "picp_vo_step must mirror VoStep");
@@ -118,17 +118,9 @@ struct picp_vo {
   // the step's gather runs inside the PICP block kernel (picp_launch_vo_block) when every frame's
   // items fit on-chip; PICP_VO_FUSE=0 keeps vo_gather_kernel + the plain block launch (A/B: the
   // same items in the same order, the same bits)
-  int fuse = 1;  // PICP_VO_FUSE: 0 separate gather, 1 gather in the PICP kernel, 2 gather + append
-  // The split world match (PICP_VO_SPLIT, default 1): step t's match of frame f0+t+1 against the
-  // map is two launches -- the EARLY part against the map as step t-2's append left it, run on
-  // the chain's early stream beside step t-1, and the LATE part against the points step t-1's
-  // append added (about one frame's new landmarks), on the chain, merged into the early part's
-  // rows (picp_match.hip match_store).  The merged top-2 is the full match's, bit for bit.
-  int split = 0;
-  std::vector<hipStream_t> estream;  // [chains]: early parts
-  std::vector<hipEvent_t> ev_app;    // [chains]: the chain's latest append (an early part may start)
-  std::vector<hipEvent_t> ev_early;  // [chains][2]: early part of step t done (by step parity)
-  hipEvent_t ev_boot = nullptr;      // the bootstrap append
+  // (the append fused after the rounds and a world match split into an early and a late part were
+  // built in round 4, bit-identical, and measured slower: DESIGN.md §4.14, commit 1ffa87f)
+  int fuse = 1;  // PICP_VO_FUSE: 0 separate gather, 1 gather in the PICP kernel
   bool guard = false;
   std::vector<VoGuarded> guards;
 #ifdef PICP_VO_DIAG
@@ -193,13 +185,6 @@ extern "C" int picp_vo_destroy(picp_vo_t* h) {
     if (e) hipEventDestroy(e);
   for (hipStream_t c : h->cstream)
     if (c) hipStreamDestroy(c);
-  for (hipEvent_t e : h->ev_app)
-    if (e) hipEventDestroy(e);
-  for (hipEvent_t e : h->ev_early)
-    if (e) hipEventDestroy(e);
-  if (h->ev_boot) hipEventDestroy(h->ev_boot);
-  for (hipStream_t c : h->estream)
-    if (c) hipStreamDestroy(c);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return PICP_OK;
@@ -254,8 +239,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   // two, round 2)
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
-  if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = std::max(0, std::min(2, atoi(e)));
-  if (const char* e = getenv("PICP_VO_SPLIT")) h->split = atoi(e) != 0;
+  if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
@@ -290,21 +274,6 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
       if (c > 0) HIP_TRY(hipStreamCreateWithPriority(&h->cstream[c], hipStreamNonBlocking, hi));
       HIP_TRY(hipEventCreateWithFlags(&h->ev_cj[c], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&h->ev_ph[c], hipEventDisableTiming));
-    }
-    if (h->split) {
-      // PICP_VO_EPRIO=0|1: the early parts' streams at the lowest / highest priority
-      const char* ee = getenv("PICP_VO_EPRIO");
-      const bool eprio_hi = !(ee && atoi(ee) == 0);
-      h->estream.assign((size_t)h->chains, nullptr);
-      h->ev_app.assign((size_t)h->chains, nullptr);
-      h->ev_early.assign((size_t)2 * h->chains, nullptr);
-      HIP_TRY(hipEventCreateWithFlags(&h->ev_boot, hipEventDisableTiming));
-      for (int c = 0; c < h->chains; ++c) {
-        HIP_TRY(hipStreamCreateWithPriority(&h->estream[c], hipStreamNonBlocking, eprio_hi ? hi : lo));
-        HIP_TRY(hipEventCreateWithFlags(&h->ev_app[c], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c + 1], hipEventDisableTiming));
-      }
     }
     return PICP_OK;
   }());
@@ -439,8 +408,6 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_stin = part((size_t)n_seg * sizeof(PicpState));
   const Part p_stout = part((size_t)n_seg * sizeof(PicpState));
   const Part p_wprobs = part((size_t)n_seg * sizeof(MatchProblem));
-  const Part p_lprobs = part((size_t)n_seg * sizeof(MatchProblem));
-  const Part p_eprobs = part((size_t)2 * n_seg * sizeof(MatchProblem));
   const Part p_pprobs = part(std::max<size_t>(pprobs.size(), 1) * sizeof(MatchProblem));
   const Part p_poses = part((size_t)n_slots * 16 * sizeof(float));
   const Part p_steps = part((size_t)n_slots * sizeof(VoStep));
@@ -514,9 +481,6 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   V.st_in = (PicpState*)(m + p_stin.off);
   V.st_out = (const PicpState*)(m + p_stout.off);
   V.wprobs = (MatchProblem*)(m + p_wprobs.off);
-  V.lprobs = (MatchProblem*)(m + p_lprobs.off);
-  V.eprobs = (MatchProblem*)(m + p_eprobs.off);
-  V.n_seg_all = n_seg;
   V.poses = (float*)(m + p_poses.off);
   V.steps = (VoStep*)(m + p_steps.off);
   V.pairs = (int2*)(m + p_pairs.off);
@@ -621,8 +585,6 @@ static hipError_t vo_enqueue(picp_vo* h) {
   }
   if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const int C = std::min(h->chains_eff, h->n_seg);
-  const bool sp = h->split && !h->estream.empty();
-  if (e == hipSuccess && sp) e = hipEventRecord(h->ev_boot, h->stream);
   // one world-match launch over this chain's segments [s0, s0 + n): tables probs (+ s0)
   auto world_match = [&](hipStream_t st, const VoArgs& V, const MatchProblem* probs) {
     return picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
@@ -660,24 +622,10 @@ static hipError_t vo_enqueue(picp_vo* h) {
       (void)s1;
       // chain c starts after chain c-1's first world match (enqueued just before, at t = 0)
       if (t == 0 && c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
-      if (sp && t == 0 && e == hipSuccess) {  // step 1's early part: the map the bootstrap left
-        hipStream_t es = h->estream[c];
-        e = hipStreamWaitEvent(es, h->ev_boot, 0);
-        if (e == hipSuccess) e = world_match(es, V, V.eprobs + (size_t)1 * h->n_seg);
-        if (e == hipSuccess) e = hipEventRecord(h->ev_early[2 * c + 1], es);
-      }
-      if (sp) {  // the late part (merged into the early part's rows; step 0: the whole map)
-        if (e == hipSuccess && t >= 1) e = hipStreamWaitEvent(st, h->ev_early[2 * c + (t & 1)], 0);
-        if (e == hipSuccess && !(skip & 8)) e = world_match(st, V, V.lprobs);
-      } else if (e == hipSuccess && !(skip & 8)) {
-        e = world_match(st, V, h->wprobs_d);
-      }
+      if (e == hipSuccess && !(skip & 8)) e = world_match(st, V, h->wprobs_d);
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
-      if (fused && h->fuse == 2) {  // the append runs in the PICP kernel: it waits for chunk t first
-        if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
-        if (e == hipSuccess) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs, 1);
-      } else if (fused) {
-        if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs, 0);
+      if (fused) {
+        if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs);
       } else {
         if (e == hipSuccess && !(skip & 1)) e = picp_launch_vo_gather(st, &V, t);
         if (e == hipSuccess && !(skip & 4))
@@ -688,25 +636,12 @@ static hipError_t vo_enqueue(picp_vo* h) {
 #ifdef PICP_VO_DIAG
       if (e == hipSuccess) e = vo_snap(h, st, t, s0, s1);
 #endif
-      if (!(fused && h->fuse == 2)) {
-        if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
-        if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
-      }
-      if (sp && t + 2 < csteps[c] && e == hipSuccess) {  // step t+2's early part: the map step t's append left
-        hipStream_t es = h->estream[c];
-        e = hipEventRecord(h->ev_app[c], st);
-        if (e == hipSuccess) e = hipStreamWaitEvent(es, h->ev_app[c], 0);
-        if (e == hipSuccess) e = world_match(es, V, V.eprobs + (size_t)((t + 2) & 1) * h->n_seg);
-        if (e == hipSuccess) e = hipEventRecord(h->ev_early[2 * c + ((t + 2) & 1)], es);
-      }
+      if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
+      if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
     }
   }
   for (int c = 1; c < C && e == hipSuccess; ++c) e = hipEventRecord(h->ev_cj[c], cst[c]);
   for (int c = 1; c < C && e == hipSuccess; ++c) e = hipStreamWaitEvent(h->stream, h->ev_cj[c], 0);  // join
-  for (int c = 0; sp && c < C && e == hipSuccess; ++c) {  // join the early streams too (a graph capture needs it)
-    e = hipEventRecord(h->ev_early[2 * c], h->estream[c]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_early[2 * c], 0);
-  }
   return e;
 }
 

@@ -62,6 +62,15 @@ def test_shipped_environment_switches_are_the_documented_ones():
     sec = doc[doc.index("## 4."):doc.index("## 5.")]
     missing = sorted(n for n in names if "`%s" % n not in sec)
     assert not missing, missing
+    # and the other way: every switch the table documents is one the library still reads (a
+    # variant removed from the library leaves no row behind)
+    documented = set()
+    for row in sec.splitlines():
+        if row.startswith("| `PICP_"):
+            documented |= set(re.findall(r"`(PICP_[A-Z0-9_]+)", row.split(" | ")[0]))
+    read = {n.decode() for n in re.findall(rb"PICP_[A-Z0-9_]+", blob)}  # any string, merged or not
+    stale = sorted(documented - read)
+    assert not stale, stale
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"), reason="no llvm-objdump")

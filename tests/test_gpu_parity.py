@@ -573,7 +573,7 @@ def test_streaming_weighted_pair_split_matches_oracle(native, oracle):
 @pytest.mark.parametrize("sizes", [[5000, 1, 3, 4097, 12000, 7], [10000] * 32, [10000] * 128])
 def test_block_split_matches_oracle(native, oracle, sizes):
     """Block mode with two or four blocks per problem (PICP_BLOCK_SPLIT=2: halves on 512-thread
-    partner blocks; =4: quarters on 256-thread blocks, two per CU -- the C4 layout at 128 frames
+    partner blocks; =4: quarters on 512-thread blocks, two per CU -- the C4 layout at 128 frames
     per GPU; partners exchange {round, hi|lo} granules every round) and with one block per
     problem: all vs the oracle, converged-round counts equal, replays bit-identical.  Problems of
     1-7 correspondences leave the later parts empty."""
@@ -610,46 +610,3 @@ def test_block_split_matches_oracle(native, oracle, sizes):
             _assert_n_in_explained(p["K"], p["xyz"], p["uv"], poses[i], T_ref, stats[i]["n_in"], st_ref["n_in"])
             if n >= 1000:
                 assert stats[i]["converged"] == int(st_ref["converged"]), (split, i)
-
-
-@pytest.mark.parametrize("P,n,split,conv", [(128, 10000, "4", -1.0), (128, 10000, "4", 1e-5), (7, 6000, "2", 1e-5),
-                                            (8, 3000, "4", -1.0), (9, 2500, "1", 1e-5), (32, 10000, "2", -1.0)])
-def test_pair_mode_bit_identical_to_block_kernel(native, oracle, P, n, split, conv):
-    """Pair mode (picp_pair.hip: two frames per block, one frame's round tail under the other's
-    linearize) against the block kernel at the same split, 512-thread parts and register items
-    per lane: the same items in the same lanes, the same sums in the same order and the same
-    finish, so the poses and stats are the same bits -- with the convergence test on, frames of a
-    pair stop at different rounds; an odd frame count leaves a pair with one frame.  Every 8th
-    frame also against the oracle; replays bit-identical (tag bases continue across launches)."""
-    import os
-    synth = _synth()
-    bt = synth.make_batch(P, n, base_seed=1700, pixel_noise=0.5, outlier_frac=0.1)
-    res = {}
-    os.environ["PICP_BLOCK_SPLIT"] = split
-    os.environ["PICP_BLOCK_NPT"] = "4"
-    try:
-        for pair in ("0", "1"):
-            os.environ["PICP_BLOCK_PAIR"] = pair
-            b = _batch_mode(native, bt["sizes"], "block")
-            assert b.info()["mode"] == "block"
-            b.set_data(bt["xyz"], bt["uv"])
-            b.set_poses(bt["T_init"])
-            b.solve(threshold=THR, max_rounds=50, conv_eps=conv)
-            poses, stats = b.poses(), b.stats()
-            b.solve(threshold=THR, max_rounds=50, conv_eps=conv)
-            np.testing.assert_array_equal(b.poses(), poses)
-            assert b.residency()["fallbacks"] == 0
-            res[pair] = (poses, stats)
-    finally:
-        for k in ("PICP_BLOCK_SPLIT", "PICP_BLOCK_NPT", "PICP_BLOCK_PAIR"):
-            os.environ.pop(k, None)
-    np.testing.assert_array_equal(res["0"][0].view(np.uint32), res["1"][0].view(np.uint32))
-    for a, c in zip(res["0"][1], res["1"][1]):
-        assert a == c
-    for i in range(0, P, 8):
-        xyz, uv = bt["xyz"][i * n:(i + 1) * n], bt["uv"][i * n:(i + 1) * n]
-        T_ref, st_ref = oracle.solve_soa(bt["T_init"][i], synth.K_REF.astype(np.float32), 480, 640,
-                                         xyz[:, 0].copy(), xyz[:, 1].copy(), xyz[:, 2].copy(),
-                                         uv[:, 0].copy(), uv[:, 1].copy(), THR, mode=oracle.MODE_F64,
-                                         max_rounds=50, conv_eps=conv)
-        assert synth.se3_log_norm(res["1"][0][i], T_ref) < POSE_TOL, i

@@ -264,10 +264,8 @@ def test_vo_step_schedules_bit_identical(native, monkeypatch):
 @pytest.mark.parametrize("obs", [600, 2000, 2300])
 def test_vo_fused_gather_bit_identical(native, monkeypatch, obs):
     """The step's gather inside the PICP block kernel (default; the items reach registers and the
-    LDS stage without the SoA planes), the append after the rounds in the same kernel
-    (PICP_VO_FUSE=2) and the split world match (PICP_VO_SPLIT=1: the older map matched beside the
-    previous step, the newest points merged into the same rows) give the separate kernels' poses,
-    step records and maps bit for bit, in the serial order and the concurrent schedule.  600 observations per frame:
+    LDS stage without the SoA planes) gives the separate kernels' poses, step records and maps bit
+    for bit, in the serial order and the concurrent schedule.  600 observations per frame:
     one register item per lane and most items in the LDS stage; 2300: four per lane, the rest in
     the stage."""
     from picp_amd.vo_synth import VOSequence, segments
@@ -278,13 +276,10 @@ def test_vo_fused_gather_bit_identical(native, monkeypatch, obs):
     rel = [np.linalg.inv(F["T_cw"][f].astype(np.float64)) for f in first]
     boot = np.stack([[np.eye(4), rel[k] @ F["T_cw"][f + 1]] for k, f in enumerate(first)]).astype(np.float32)
     ref = None
-    for env in ({"PICP_VO_FUSE": "0", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1", "PICP_VO_SPLIT": "0"},
-                {"PICP_VO_FUSE": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1", "PICP_VO_SPLIT": "0"},
-                {"PICP_VO_FUSE": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1", "PICP_VO_SPLIT": "1"},
-                {"PICP_VO_FUSE": "2", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1", "PICP_VO_SPLIT": "0"},
-                {"PICP_VO_FUSE": "2", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None, "PICP_VO_SPLIT": None},
-                {"PICP_VO_FUSE": None, "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None, "PICP_VO_SPLIT": "0"},
-                {"PICP_VO_FUSE": None, "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None, "PICP_VO_SPLIT": None}):
+    for env in ({"PICP_VO_FUSE": "0", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
+                {"PICP_VO_FUSE": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
+                {"PICP_VO_FUSE": "0", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None},
+                {"PICP_VO_FUSE": None, "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None}):
         for k, v in env.items():
             if v is None:
                 monkeypatch.delenv(k, raising=False)
