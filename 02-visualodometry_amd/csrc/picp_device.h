@@ -865,7 +865,13 @@ namespace picp {
 // most a register copy per move.
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
+#ifdef PICP_DPP_MOV  // A/B: round 3's form (old undefined; every call site runs with EXEC full)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+#elif defined(PICP_DPP_BC)  // A/B: bound_ctrl on, old unused (a disabled source lane reads 0)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+#else
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+#endif
 }
 #define DPP_ROW_MIRROR 0x140
 #define DPP_ROW_HALF_MIRROR 0x141
@@ -1096,7 +1102,9 @@ __device__ __forceinline__ void taylor_sincos(float a, float* s, float* c) {
 __device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3]) {
   // every product rounded before its sum, whatever code surrounds the inlined update: the
   // compiler may not choose which of a*b + c*d to fuse
+#ifndef PICP_UPDATE_CONTRACT
 #pragma clang fp contract(off)
+#endif
   float sa, ca, sb, cb, sc, cc;
   if (fabsf(dx[3]) <= 0.0625f && fabsf(dx[4]) <= 0.0625f && fabsf(dx[5]) <= 0.0625f) {
     taylor_sincos(dx[3], &sa, &ca);
@@ -1124,7 +1132,9 @@ __device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3
 // src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
 // src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
 __device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
+#ifndef PICP_UPDATE_CONTRACT
 #pragma clang fp contract(off)  // products rounded, then summed in order (as the oracle)
+#endif
   float Rd[3][3];
   update_rotation(dx, Rd);
   float Rn[9], tn[3];
