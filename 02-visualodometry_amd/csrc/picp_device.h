@@ -859,19 +859,13 @@ namespace picp {
 // Cross-lane moves without the LDS crossbar.  gfx950 v_permlane32_swap / v_permlane16_swap
 // exchange half-waves / odd-even 16-lane rows between two registers; DPP reads a partner
 // lane inside a 16-lane row (row_mirror l^15, row_half_mirror l^7, quad_perm l^2, l^1).
-// The lane's own value is the DPP "old" operand: with bound_ctrl off, a lane whose source lane is
-// disabled in EXEC keeps old instead of an undefined register (mov_dpp leaves it undefined).  Every
-// call site runs with EXEC full, so the results are the same either way; the defined form costs at
-// most a register copy per move.
+// bound_ctrl on: a lane whose source lane is disabled in EXEC reads 0, so the result never depends
+// on the destination's old contents (every call site runs with EXEC full, where no source lane is
+// disabled).  Passing the source as DPP "old" instead (round 4) tied the destination to it and
+// cost a register copy per move: C2/C3 1-2 % slower in interleaved A/B (profiles/r05/ab_regress/).
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-#ifdef PICP_DPP_MOV  // A/B: round 3's form (old undefined; every call site runs with EXEC full)
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-#elif defined(PICP_DPP_BC)  // A/B: bound_ctrl on, old unused (a disabled source lane reads 0)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-#else
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
-#endif
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 #define DPP_ROW_MIRROR 0x140
 #define DPP_ROW_HALF_MIRROR 0x141
@@ -1100,11 +1094,6 @@ __device__ __forceinline__ void taylor_sincos(float a, float* s, float* c) {
 
 // src/defs.h:100-136 v2tEuler's rotation: Rd = Rx(a)*Ry(b)*Rz(c) (float) of dx[3..5].
 __device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3]) {
-  // every product rounded before its sum, whatever code surrounds the inlined update: the
-  // compiler may not choose which of a*b + c*d to fuse
-#ifndef PICP_UPDATE_CONTRACT
-#pragma clang fp contract(off)
-#endif
   float sa, ca, sb, cb, sc, cc;
   if (fabsf(dx[3]) <= 0.0625f && fabsf(dx[4]) <= 0.0625f && fabsf(dx[5]) <= 0.0625f) {
     taylor_sincos(dx[3], &sa, &ca);
@@ -1132,9 +1121,8 @@ __device__ __forceinline__ void update_rotation(const float dx[6], float Rd[3][3
 // src/defs.h:100-136 v2tEuler: R = Rx(a)*Ry(b)*Rz(c) (float), t = v[0:3]; then
 // src/picp_solver.cpp:103 T <- v2tEuler(dx) * T.
 __device__ __forceinline__ void apply_update(const float dx[6], float R[9], float t[3]) {
-#ifndef PICP_UPDATE_CONTRACT
-#pragma clang fp contract(off)  // products rounded, then summed in order (as the oracle)
-#endif
+  // (round 4 pinned the contractions here with fp contract(off) for a fused append that is gone;
+  // it cost C2/C3 1-2 % -- profiles/r05/ab_regress/ -- and parity does not depend on it)
   float Rd[3][3];
   update_rotation(dx, Rd);
   float Rn[9], tn[3];

@@ -4,6 +4,20 @@
 
 #include "picp_c.h"
 
+// the descriptor matcher's launchers (picp_match.hip)
+extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* desc, int64_t n, int dim,
+                                             _Float16* h, float* n1, float* n2);
+extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
+                                             const float* q_desc, const float* r_desc,
+                                             const _Float16* q_h, const float* q_n1,
+                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
+                                             const struct MatchProblem* probs, int dim, float dist_thr,
+                                             float ratio_thr, int32_t* best_idx, float* best_dist,
+                                             float* second_dist, int32_t* accepted, int form, int ksplit,
+                                             float4* part);
+extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int form);
+extern "C" int picp_match_prep_kch(int dim);
+
 // records the thread's last error message (picp_last_error) and returns `code`
 __attribute__((visibility("hidden"), format(printf, 2, 3))) int picp_set_err(int code, const char* fmt, ...);
 

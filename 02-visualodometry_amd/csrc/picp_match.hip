@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "picp_internal.h"
 
 #define PICP_MATCH_BLOCK 256
@@ -154,6 +156,18 @@ typedef float mm_f16v __attribute__((ext_vector_type(16)));
 // The launcher takes RB = 2 when that still fills a generation of blocks (C5: +3.4 %,
 // 1024 x 2000 x 2000: -9 % time) and RB = 1 for small grids (64 x 2000 x 8000: RB = 2 +9 %).
 #define MM_CAP 16                 // candidate slots per query
+// Reference-range split (ksplit > 1): a problem's references in ranges of mm_kchunk rows, at least
+// MM_KMIN (so a range is worth a block's query prologue), whole tiles; mm_nsplit non-empty ranges.
+#define MM_KMIN 1024
+#define MM_KSPLIT_MAX 16
+__host__ __device__ __forceinline__ int64_t mm_kchunk(int64_t nr, int ksplit) {
+  const int64_t c = (nr + ksplit - 1) / ksplit;
+  const int64_t t = (c + 255) / 256 * 256;
+  return t > MM_KMIN ? t : MM_KMIN;
+}
+__host__ __device__ __forceinline__ int mm_nsplit(int64_t nr, int ksplit) {
+  return nr > 0 ? (int)((nr + mm_kchunk(nr, ksplit) - 1) / mm_kchunk(nr, ksplit)) : 0;
+}
 #define MM_SAFE 60000.0f
 
 __device__ __forceinline__ float mm_bound(float nq, float rmax) {
@@ -357,7 +371,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const MatchProblem* __restrict__ probs, int dim, float dist_thr, float ratio_thr,
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
     float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
-    int xcd_map) {
+    int xcd_map, int ksplit, float4* __restrict__ part, int64_t part_nq) {
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
@@ -386,18 +400,32 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   // 8 XCDs, so block L runs beside blocks L +- 8.  With xcd_map, problem p's query blocks all
   // get L = p (mod 8): every block of a problem shares one XCD's L2, which then holds the
   // references of the ~10 problems in flight there instead of a slice of all of them.
-  int pid, qblk;
+  // With ksplit > 1 (mm_ksplit), group g = pid * ksplit + ks holds the query blocks of problem pid
+  // against the ks-th contiguous range of its references (mm_kchunk); the groups take the place of
+  // the problems in the XCD map (the blocks that read one reference range share an L2).
+  int pid, qblk, ks = 0;
   if (xcd_map) {
     const unsigned L = blockIdx.x, x = L & 7u, sidx = L >> 3;
     const unsigned pq = sidx / (unsigned)gx;
     qblk = (int)(sidx - pq * (unsigned)gx);
-    pid = (int)(pq * 8u + x);
+    const unsigned g = pq * 8u + x;
+    pid = (int)(g / (unsigned)ksplit);
+    ks = (int)(g - (unsigned)pid * (unsigned)ksplit);
     if (pid >= n_problems) return;
   } else {
     pid = blockIdx.y;
-    qblk = blockIdx.x;
+    qblk = blockIdx.x % gx;
+    ks = blockIdx.x / gx;
   }
-  const MatchProblem P = probs[pid];
+  MatchProblem P = probs[pid];
+  int64_t r_lo = 0;  // this block's references: [r_lo, r_lo + P.nr) of the problem's (P is local)
+  if (ksplit > 1) {
+    const int64_t kc = mm_kchunk(P.nr, ksplit);
+    r_lo = (int64_t)ks * kc;
+    if (r_lo >= P.nr) return;  // an empty range (the merge reads only mm_nsplit ranges)
+    P.r_off += r_lo;
+    P.nr = min(kc, P.nr - r_lo);
+  }
   const int64_t q0 = (int64_t)qblk * QPB;
   if (q0 >= P.nq) return;  // whole block past this problem
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
@@ -821,9 +849,46 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
       }
     }
-    match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                accepted);  // :100-103
+    if (ksplit > 1)  // this range's top-2 (global index), merged in range order by picp_match_merge_kernel
+      part[((int64_t)ks * n_problems + pid) * part_nq + qi] =
+          make_float4(__int_as_float(bi >= 0 ? (int32_t)(bi + r_lo) : -1), best, second, 0.0f);
+    else
+      match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                  accepted);  // :100-103
   }
+}
+
+// The reference ranges of a split launch, merged in index order: the reference's in-order
+// strict-'<' scan over range 0, then range 1, ... yields best = the smaller best (a tie keeps the
+// earlier range's, i.e. the lower index), second = the second smallest of the union.  Each range's
+// (best, first index, second) is exactly its own in-order scan's (index-order-independent update
+// above), so the merged triple is the whole scan's.  One thread per query.
+extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, int n_problems,
+                                                   int ksplit, const float4* __restrict__ part, int64_t part_nq,
+                                                   float dist_thr, float ratio_thr, int32_t* __restrict__ best_idx,
+                                                   float* __restrict__ best_dist, float* __restrict__ second_dist,
+                                                   int32_t* __restrict__ accepted) {
+  const int pid = blockIdx.y;
+  const MatchProblem P = probs[pid];
+  const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= P.nq) return;
+  const int ns = mm_nsplit(P.nr, ksplit);
+  float best = FLT_MAX, second = FLT_MAX;  // src/my_utilities.h:78-79
+  int32_t bi = -1;
+  for (int k = 0; k < ns; ++k) {
+    const float4 r = part[((int64_t)k * n_problems + pid) * part_nq + qi];
+    const float b = r.y;
+    if (b < best) {
+      second = fminf(best, r.z);
+      best = b;
+      bi = __float_as_int(r.x);
+    } else if (b == best) {
+      second = best;  // two equal values in the multiset; the earlier index stays
+    } else {
+      second = fminf(second, b);
+    }
+  }
+  match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted);
 }
 
 extern "C" int picp_match_prep_kch(int dim) { return dim <= 16 ? 1 : 2; }
@@ -848,8 +913,10 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const _Float16* r_h, const float* r_n1, const float* r_n2,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int form) {
+                                             float* second_dist, int32_t* accepted, int form, int ksplit,
+                                             float4* part) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
+  if (ksplit < 1 || ksplit > MM_KSPLIT_MAX || (ksplit > 1 && !part)) return hipErrorInvalidValue;
   const bool accept_only = (form & 1) != 0;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
   // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
@@ -878,11 +945,14 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   const int gx = (int)((max_nq + qpb - 1) / qpb);
   const char* xe = getenv("PICP_MATCH_XCD");
   const int xcd_map = (xe && atoi(xe) == 0) ? 0 : 1;
-  const dim3 g = xcd_map ? dim3((unsigned)(8 * ((n_problems + 7) / 8) * gx)) : dim3((unsigned)gx, (unsigned)n_problems);
+  const int64_t ngroups = (int64_t)n_problems * ksplit;
+  const dim3 g = xcd_map ? dim3((unsigned)(8 * ((ngroups + 7) / 8) * gx))
+                         : dim3((unsigned)(gx * ksplit), (unsigned)n_problems);
+  const int64_t part_nq = max_nq;
 #define PICP_LAUNCH_MM3(KC, RD, R)                                                                          \
   hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD, R>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h,  \
                      q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, \
-                     accepted, n_problems, gx, xcd_map)
+                     accepted, n_problems, gx, xcd_map, ksplit, part, part_nq)
 #define PICP_LAUNCH_MM(KC, RD)                   \
   {                                              \
     if (rb == 2) PICP_LAUNCH_MM3(KC, RD, 2);     \
@@ -898,7 +968,35 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   }
 #undef PICP_LAUNCH_MM3
 #undef PICP_LAUNCH_MM
+  if (ksplit > 1) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(picp_match_merge_kernel, dim3((unsigned)((max_nq + 255) / 256), (unsigned)n_problems),
+                       dim3(256), 0, stream, probs, n_problems, ksplit, (const float4*)part, part_nq, dist_thr,
+                       ratio_thr, best_idx, best_dist, second_dist, accepted);
+  }
   return hipGetLastError();
+}
+
+// The reference-range split a launch of this shape takes (1: none): enough (problem, query block,
+// range) blocks for about four per CU, at most MM_KSPLIT_MAX ranges.  The caller provides
+// ksplit x n_problems x max_nq float4 of scratch (picp_launch_match_mfma's part) when > 1.
+// PICP_MATCH_KSPLIT=n forces n (1: no split; A/B).  Small problem counts against large reference
+// sets (the VO world match of a few long segments: 8 x 2,000 queries x ~1.9e5 map points) would
+// otherwise run one block per CU or fewer.
+extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int form) {
+  if (form & 2) return 1;  // the exact scan is not split
+  static int num_cu = 0;
+  if (!num_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cu <= 0)
+      num_cu = 256;
+  }
+  const int64_t base = (int64_t)n_problems * ((max_nq + 32 * MM_WAVES - 1) / (32 * MM_WAVES));
+  int64_t k = (4 * (int64_t)num_cu + base - 1) / std::max<int64_t>(base, 1);
+  if (const char* e = getenv("PICP_MATCH_KSPLIT")) k = atoi(e);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(k, MM_KSPLIT_MAX));
 }
 
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,

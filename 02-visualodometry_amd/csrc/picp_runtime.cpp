@@ -53,16 +53,6 @@ extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int6
                                         const MatchProblem* probs, int dim, float dist_thr,
                                         float ratio_thr, int32_t* best_idx, float* best_dist,
                                         float* second_dist, int32_t* accepted);
-extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* desc, int64_t n, int dim,
-                                             _Float16* h, float* n1, float* n2);
-extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
-                                             const float* q_desc, const float* r_desc,
-                                             const _Float16* q_h, const float* q_n1,
-                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
-                                             const MatchProblem* probs, int dim, float dist_thr,
-                                             float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int form);
-extern "C" int picp_match_prep_kch(int dim);
 extern "C" __global__ void picp_rcp_check_kernel(int e_lo, int e_hi, unsigned long long* bad);
 extern "C" hipError_t picp_launch_essential(hipStream_t stream, const EssArgs* args, const int64_t* offs,
                                            const float* p1, const float* p2, int32_t* idx, double* Es,
@@ -1515,8 +1505,11 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   const int dp = 16 * picp_match_prep_kch(dim);
   const size_t n2a = (size_t)std::max<int64_t>(n2, 1);
   const size_t b_prep = ((size_t)n1 + n2a) * (dp * sizeof(_Float16) + 2 * sizeof(float));
+  // the reference-range split's scratch (picp_match_ksplit: few problems against many references)
+  const int ks = picp_match_ksplit(n_problems, max_nq, form);
+  const size_t b_part = ks > 1 ? (size_t)ks * n_problems * max_nq * sizeof(float4) : 0;
   char* buf = nullptr;
-  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + 256));
+  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + b_part + 512));
   char* cur = buf;
   auto carve = [&](size_t bytes) { char* r = cur; cur += (bytes + 15) / 16 * 16; return r; };
   MatchProblem* d_probs = (MatchProblem*)carve(b_probs);
@@ -1532,6 +1525,7 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   _Float16* r_h = (_Float16*)carve(n2a * dp * sizeof(_Float16));
   float* r_n1 = (float*)carve(n2a * 4);
   float* r_n2 = (float*)carve(n2a * 4);
+  float4* d_part = ks > 1 ? (float4*)carve(b_part) : nullptr;
   hipError_t e = hipMemcpy(d_probs, probs.data(), b_probs, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_d1, desc1, b_d1, hipMemcpyHostToDevice);
   if (e == hipSuccess && n2) e = hipMemcpy(d_d2, desc2, (size_t)n2 * dim * sizeof(float), hipMemcpyHostToDevice);
@@ -1539,7 +1533,7 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)
     e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
-                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form);
+                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form, ks, d_part);
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);

@@ -21,16 +21,6 @@
 #include "picp_host.h"
 #include "picp_internal.h"
 
-extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* desc, int64_t n, int dim,
-                                             _Float16* h, float* n1, float* n2);
-extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
-                                             const float* q_desc, const float* r_desc,
-                                             const _Float16* q_h, const float* q_n1,
-                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
-                                             const MatchProblem* probs, int dim, float dist_thr,
-                                             float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int form);
-extern "C" int picp_match_prep_kch(int dim);
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
@@ -115,6 +105,12 @@ struct picp_vo {
   std::vector<hipEvent_t> ev_cj;     // [chains]: group c's end (join), [0]: fork
   std::vector<hipEvent_t> ev_ph;     // [chains]: group c's first world match done
   int accept_only = 1;  // the sequence reads only accepted matches (PICP_VO_MATCH_FULL=1: full form)
+  // the matcher's reference-range split (picp_match_ksplit) for launches of few problems: each
+  // chain's world match has its own scratch (the chains run concurrently), the frame->next
+  // launches one between them (they run in stream order: chunk 0, then the side stream's)
+  std::vector<int> ks_w;          // [chains]
+  std::vector<float4*> part_w;    // [chains]
+  float4* part_p = nullptr;
   // the step's gather runs inside the PICP block kernel (picp_launch_vo_block) when every frame's
   // items fit on-chip; PICP_VO_FUSE=0 keeps vo_gather_kernel + the plain block launch (A/B: the
   // same items in the same order, the same bits)
@@ -415,6 +411,27 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_mh = part((size_t)map_slots * h->dp * sizeof(_Float16));
   const Part p_mn1 = part((size_t)map_slots * sizeof(float));
   const Part p_mn2 = part((size_t)map_slots * sizeof(float));
+  // split scratch: each chain's world match (its n_seg_c problems) and the frame->next launches
+  std::vector<int> ks_w((size_t)chains_eff, 1);
+  std::vector<Part> p_partw;
+  for (int c = 0; c < chains_eff; ++c) {
+    const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
+    ks_w[c] = picp_match_ksplit(nsc, h->max_obs, h->accept_only);
+    p_partw.push_back(part(ks_w[c] > 1 ? (size_t)ks_w[c] * nsc * h->max_obs * sizeof(float4) : 0));
+  }
+  size_t part_p_bytes = 0;
+  {
+    auto need = [&](size_t np) {
+      for (size_t q = 0; q < np; q += VO_MAX_GRID_Y) {
+        const int n = (int)std::min<size_t>(VO_MAX_GRID_Y, np - q);
+        const int k = picp_match_ksplit(n, h->max_obs, h->accept_only);
+        if (k > 1) part_p_bytes = std::max(part_p_bytes, (size_t)k * n * h->max_obs * sizeof(float4));
+      }
+    };
+    need(pprobs.size());  // the frame->next matches up front (overlap off)
+    for (size_t k = 0; k + 1 < chunk_off.size(); ++k) need(chunk_off[k + 1] - chunk_off[k]);
+  }
+  const Part p_partp = part(part_p_bytes);
   HIP_TRY(vo_malloc(h, &h->seg_mem, total, "segments"));
   HIP_TRY(hipMemset(h->seg_mem, 0, total));  // every table defined before the first run
   char* m = (char*)h->seg_mem;
@@ -422,6 +439,11 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   for (auto& e : h->ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   h->chunk_off = chunk_off;
   h->chains_eff = chains_eff;
+  h->ks_w = ks_w;
+  h->part_w.assign((size_t)chains_eff, nullptr);
+  for (int c = 0; c < chains_eff; ++c)
+    if (p_partw[c].bytes) h->part_w[c] = (float4*)(m + p_partw[c].off);
+  h->part_p = part_p_bytes ? (float4*)(m + p_partp.off) : nullptr;
   h->segs = segs;
   h->pprobs = pprobs;
   h->n_seg = n_seg;
@@ -501,9 +523,10 @@ static hipError_t vo_frame_match(picp_vo* h, hipStream_t st, size_t p0, size_t p
   hipError_t e = hipSuccess;
   for (; p0 < p1 && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
     const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - p0);
+    const int ks = h->part_p ? picp_match_ksplit(np, h->max_obs, h->accept_only) : 1;
     e = picp_launch_match_mfma(st, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1, h->obs_h,
                                h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
-                               h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only);
+                               h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only, ks, h->part_p);
   }
   return e;
 }
@@ -585,11 +608,12 @@ static hipError_t vo_enqueue(picp_vo* h) {
   }
   if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const int C = std::min(h->chains_eff, h->n_seg);
-  // one world-match launch over this chain's segments [s0, s0 + n): tables probs (+ s0)
-  auto world_match = [&](hipStream_t st, const VoArgs& V, const MatchProblem* probs) {
+  // one world-match launch over chain c's segments [s0, s0 + n): tables probs (+ s0)
+  auto world_match = [&](hipStream_t st, const VoArgs& V, const MatchProblem* probs, int c) {
     return picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
                                   V.map_n1, V.map_n2, probs + V.seg0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
-                                  h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only);
+                                  h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only,
+                                  h->part_w[c] ? h->ks_w[c] : 1, h->part_w[c]);
   };
 #ifdef PICP_VO_DIAG
   const bool fused = false;  // vo_snap and PICP_VO_DIAG_SKIP need the gather's planes and launch
@@ -622,7 +646,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
       (void)s1;
       // chain c starts after chain c-1's first world match (enqueued just before, at t = 0)
       if (t == 0 && c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
-      if (e == hipSuccess && !(skip & 8)) e = world_match(st, V, h->wprobs_d);
+      if (e == hipSuccess && !(skip & 8)) e = world_match(st, V, h->wprobs_d, c);
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
       if (fused) {
         if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs);

@@ -164,3 +164,29 @@ def test_match_batch_two_row_blocks(native, oracle, monkeypatch):
     outs = native.match_points_batch(d1s, d2s)
     for d1, d2, got in zip(d1s, d2s, outs):
         _eq(got, oracle.match_points(d1, d2))
+
+
+@pytest.mark.parametrize("ksplit", ["1", "3", "5", "16"])
+def test_match_reference_range_split(native, oracle, monkeypatch, ksplit):
+    """The reference-range split (picp_match_ksplit: few problems against many references, e.g.
+    the VO world match of a few long segments): each range's top-2 is merged in range order
+    (picp_match_merge_kernel).  PICP_MATCH_KSPLIT forces the range count; ranges are >= 1,024 rows,
+    so 5,000 references make up to 5.  Exact duplicates on both sides of range boundaries (the
+    lower index must win and second = best), a triple duplicate across three ranges, near-ties
+    across a boundary, and a ragged batch with empty sets."""
+    monkeypatch.setenv("PICP_MATCH_KSPLIT", ksplit)
+    rng = np.random.default_rng(77)
+    d2 = rng.uniform(-1, 1, (5000, 10)).astype(np.float32)
+    d2[1024] = d2[1023]                                   # boundary of ranges 0 | 1
+    d2[2048] = d2[4000] = d2[2047]                        # across ranges 1 | 2 | 3
+    d2[3072] = d2[3071] + np.float32(1e-4)                # near-tie across 2 | 3
+    d1 = np.concatenate([d2[[1023, 1024, 2047, 3071, 3072, 4999, 0]] + 0.0,
+                         d2[rng.choice(5000, 600, replace=False)] + rng.normal(0, 0.01, (600, 10)).astype(np.float32),
+                         rng.uniform(-1, 1, (300, 10)).astype(np.float32)])
+    _eq(native.match_points(d1, d2), oracle.match_points(d1, d2))
+    sizes = [(0, 5), (40, 0), (700, 5000), (1, 1), (0, 0), (300, 2100)]
+    d1s, d2s = zip(*[_sets(rng, a, b, 10) for a, b in sizes])
+    d1s, d2s = list(d1s), list(d2s)
+    d1s[2], d2s[2] = d1[:700], d2
+    for d1_, d2_, got in zip(d1s, d2s, native.match_points_batch(d1s, d2s)):
+        _eq(got, oracle.match_points(d1_, d2_))
