@@ -23,7 +23,12 @@ Sub-results on the same line (default run, bounded time):
 Each carries value, ms_per_step, the dominant kernel's launch time, its committed PMC traffic
 (profiles/) and, at N = 1, the oracle's CPU baseline on a bounded sample.
 
-Printed JSON also carries:
+The printed line is compact (< 2 KB: the driver keeps only the tail of stdout): the contract's
+keys first, then each sub-result's value, step time, roofline fraction and projections
+(compact_line).  The full result -- every sample, basis string and sub-result -- goes to the side
+file named by "detail" (default gpurun_out/bench_detail_<workload>_n<N>.json).
+
+The full result also carries:
   roofline     : the dominant kernel of the headline (picp_persistent_kernel: the whole 50-round
                  solve in one launch); achieved = 20 algorithmic bytes per correspondence-round
                  (x,y,z,u,v float32 SoA) x correspondence-rounds per launch / mean launch period,

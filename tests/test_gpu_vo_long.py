@@ -32,6 +32,22 @@ THR = 3000.0
 POSE_TOL = 1e-4
 
 
+def _iso_inverse_f32(T):
+    """Eigen::Isometry3f::inverse() of a camera-in-world pose in float32, in the order the GPU's
+    append computes the next step's prior (picp_vo_device.h vo_iso_inverse, contraction off):
+    R^T, and -(R^T t) summed k = 0, 1, 2 with every product and sum rounded to float32."""
+    R = np.asarray(T, np.float32)[:3, :3]
+    t = np.asarray(T, np.float32)[:3, 3]
+    out = np.eye(4, dtype=np.float32)
+    out[:3, :3] = R.T
+    for i in range(3):
+        s = np.float32(R[0, i] * t[0])
+        s = np.float32(s + np.float32(R[1, i] * t[1]))
+        s = np.float32(s + np.float32(R[2, i] * t[2]))
+        out[i, 3] = -s
+    return out
+
+
 def _se3_cw(a, b):
     from picp_amd.synth import se3_log_norm, rigid_inverse
     return se3_log_norm(rigid_inverse(np.asarray(a, np.float64)), rigid_inverse(np.asarray(b, np.float64)))
@@ -78,7 +94,10 @@ def test_vo_8e_segment_teacher_forced_late_steps(oracle, segment_8e, t):
     wm = oracle.match_points(dn, md[:m])
     assert int(wm["accepted"].sum()) == int(R["n_corr"][t + 1])
     pairs = np.stack([np.nonzero(wm["accepted"])[0], wm["best_idx"][wm["accepted"]]], 1).astype(np.int32)
-    T0 = np.linalg.inv(P[t].astype(np.float64)).astype(np.float32)
+    # the step's prior exactly as the GPU formed it: the float32 inverse of its pose of frame t
+    # (exec/icp_test.cpp:77-78); late in a drifted segment a one-ulp change of the prior moves the
+    # result by ~1e-4, so a prior inverted in float64 and rounded would not be this step's input
+    T0 = _iso_inverse_f32(P[t])
     img = uv[off[nf]:off[nf + 1]]
     T, st = oracle.solve(T0, K, 480, 640, mx[:m], img, pairs, THR)
     err = _se3_cw(np.linalg.inv(T.astype(np.float64)), P[t + 1])
