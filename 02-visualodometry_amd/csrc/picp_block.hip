@@ -25,8 +25,6 @@
 // below says every block is resident at once.
 // split = 4 runs two 512-thread blocks per CU from DIFFERENT problems (<= 128 VGPRs each): while
 // one problem's parts exchange and solve (the CU idle in split = 2), the other's compute.
-// split = 8 (PICP_BLOCK_SPLIT=8, A/B) runs four 256-thread blocks per CU (one wave per SIMD each,
-// <= 128 VGPRs): three other problems' parts to hide each part's round tail.
 #include <type_traits>
 
 #include "picp_vo_device.h"
@@ -38,7 +36,6 @@ using namespace picp;
 // partner polls run back to back: an s_sleep 1 between polls measured C4 1704-1711 us vs
 // 1700-1706 us without it, 4 of 4 interleaved reps (profiles/r02/e4/ab_bspin.log).
 #define PICP_XG 64            // exchange granules per block per round: 32 hi + 32 lo
-#define PICP_SPLIT_MAX 8
 
 typedef __attribute__((address_space(1))) unsigned long long bgu64_t;
 
@@ -426,23 +423,22 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long deadline = __builtin_amdgcn_s_memrealtime() + timeout_ticks;
         const unsigned g0 = ((blockIdx.x >> 3) / (unsigned)split) * (unsigned)split;  // part 0's group
-        // partners held in registers: up to 8 for the 256-thread split-8 parts, 4 otherwise
-        constexpr int SPM = (BS == 256) ? PICP_SPLIT_MAX : 4;
-        double part_t[SPM];
+        double part_t[4];
         unsigned pending = 0;
 #pragma unroll
-        for (int q = 0; q < SPM; ++q) {
-          part_t[q] = (q == h) ? (double)hi + (double)lo : 0.0;
+        for (int q = 0; q < 4; ++q) {
+          part_t[q] = 0.0;
           if (q < split && q != h) pending |= 1u << q;
         }
+        part_t[h & 3] = (double)hi + (double)lo;
         for (;;) {
           // every partner's two granules loaded before any tag is checked (the partners are a
           // block-uniform set, so the loads issue back to back): one round trip per poll.  Checking
           // each partner right after its loads (round 3's form) waited one round trip per
           // partner, three per poll at split 4.
-          unsigned long long gh[SPM], gl[SPM];
+          unsigned long long gh[4], gl[4];
 #pragma unroll
-          for (int q = 0; q < SPM; ++q) {
+          for (int q = 0; q < 4; ++q) {
             gh[q] = gl[q] = 0ull;
             if (q < split && q != h) {
               const bgu64_t* theirs = xgg + (slot + (((g0 + q) << 3) | (blockIdx.x & 7u))) * PICP_XG;
@@ -451,7 +447,7 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
             }
           }
 #pragma unroll
-          for (int q = 0; q < SPM; ++q) {
+          for (int q = 0; q < 4; ++q) {
             if ((pending & (1u << q)) && (unsigned)(gh[q] >> 32) == tag && (unsigned)(gl[q] >> 32) == tag) {
               part_t[q] = (double)__uint_as_float((unsigned)gh[q]) + (double)__uint_as_float((unsigned)gl[q]);
               pending &= ~(1u << q);
@@ -466,7 +462,7 @@ __global__ __launch_bounds__(BS, MINW) void picp_block_kernel(
         }
         t = part_t[0];
 #pragma unroll
-        for (int q = 1; q < SPM; ++q)
+        for (int q = 1; q < 4; ++q)
           if (q < split) t += part_t[q];
       }
       s_tot[tid] = total_word(A, tid, t);  // lane e converts total e
@@ -508,36 +504,34 @@ extern "C" int picp_block_max_items(void) { return 8 * PICP_BBLOCK; }  // regist
 // Threads per block: 512 for every split; split 4 runs two blocks per CU (two waves per SIMD each,
 // <= 128 VGPRs: MINW 4).  256-thread split-4 parts (round 1) measured 5-7 % slower
 // (profiles/r01/c4_split4_ab.log, profiles/r04/c4_128/).
-extern "C" int picp_block_threads(int split) { return (split == 8) ? 256 : PICP_BBLOCK; }
+extern "C" int picp_block_threads(int split) { return (void)split, PICP_BBLOCK; }
 
 // dynamic LDS of a launch: the part of a problem (or of its 1/split share) past the
 // register-resident npt x BS items, capped by the stage
 static size_t block_lds_bytes(int npt, int split, int max_n, int* lds_items_out) {
   const int per_block = (split > 1) ? ((((max_n + split - 1) / split) + 3) & ~3) : max_n;
   const int bs = picp_block_threads(split);
-  // two (split 4) or four (split 8) blocks share a CU's LDS
-  const int lds_cap = (split == 8) ? PICP_BLDS_ITEMS / 4 : (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;
+  const int lds_cap = (split == 4) ? PICP_BLDS_ITEMS / 2 : PICP_BLDS_ITEMS;  // two blocks share a CU's LDS
   const int lds_items = (per_block > npt * bs) ? min(per_block - npt * bs, lds_cap) : 0;
   if (lds_items_out) *lds_items_out = lds_items;
   return (size_t)5 * lds_items * sizeof(float);
 }
 
-// the kernel of a launch: waves per SIMD 2 (split 1, 2), split 4's 4 (two 512-thread blocks) or
-// split 8's 4 (four 256-thread blocks)
-template <int N, int W, int BS = PICP_BBLOCK>
+// the kernel of a launch: waves per SIMD 2 (split 1, 2) or split 4's 4
+template <int N, int W>
 static const void* block_kernel_nw(int var) {
   switch (var) {
-    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, BS, NoVo, W>;
-    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, BS, NoVo, W>;
-    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, BS, NoVo, W>;
+    case PICP_V_PINHOLE: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE, PICP_BBLOCK, NoVo, W>;
+    case PICP_V_PINHOLE_KEEP: return (const void*)picp_block_kernel<N, PICP_V_PINHOLE_KEEP, PICP_BBLOCK, NoVo, W>;
+    default: return (const void*)picp_block_kernel<N, PICP_V_GENERAL, PICP_BBLOCK, NoVo, W>;
   }
 }
 
 template <int N>
 static const void* block_kernel_n(int var, int split) {
-  if (split == 4 || split == 8) {
-    if constexpr (N <= 4) return (split == 8) ? block_kernel_nw<N, 4, 256>(var) : block_kernel_nw<N, 4>(var);
-    return nullptr;  // <= 128 VGPRs: NPT <= 4
+  if (split == 4) {
+    if constexpr (N <= 4) return block_kernel_nw<N, 4>(var);  // <= 128 VGPRs: NPT <= 4
+    return nullptr;
   }
   return block_kernel_nw<N, 2>(var);
 }
@@ -552,8 +546,8 @@ static const void* block_kernel_ptr(int npt, int var, int split) {
   }
 }
 
-// Register items per lane the split-4 / split-8 layouts allow (their 128-VGPR budget); 8 otherwise.
-extern "C" int picp_block_npt_cap(int split) { return (split >= 4) ? 4 : 8; }
+// Register items per lane the split-4 layout allows (its 128-VGPR budget); 8 otherwise.
+extern "C" int picp_block_npt_cap(int split) { return (split == 4) ? 4 : 8; }
 
 // Blocks of the variants a launch with these arguments may use that one CU holds at once (the
 // hardware limit from registers, LDS and waves; other work on the device is not counted; the
@@ -561,7 +555,7 @@ extern "C" int picp_block_npt_cap(int split) { return (split >= 4) ? 4 : 8; }
 // multiplies by the CU count and launches a split grid (whose blocks wait on each other) only if
 // the whole grid fits.
 extern "C" hipError_t picp_block_occupancy(int npt, int split, int max_n, const float K[9], int* blocks_per_cu) {
-  if (!blocks_per_cu || (split != 1 && split != 2 && split != 4 && split != 8)) return hipErrorInvalidValue;
+  if (!blocks_per_cu || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
   const int bs = picp_block_threads(split);
   const size_t lds_bytes = block_lds_bytes(npt, split, max_n, nullptr);
   int best = -1;
@@ -594,7 +588,7 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         PicpState* st_out, int max_n, int split,
                                         unsigned long long* xg, unsigned int* err,
                                         unsigned int* tagbase, unsigned long long timeout_ticks) {
-  if (n_problems <= 0 || !args || (split != 1 && split != 2 && split != 4 && split != 8)) return hipErrorInvalidValue;
+  if (n_problems <= 0 || !args || (split != 1 && split != 2 && split != 4)) return hipErrorInvalidValue;
   if (split > 1 && (!xg || !err || !tagbase)) return hipErrorInvalidValue;
   const int grid = (split > 1) ? ((split * n_problems + 8 * split - 1) / (8 * split)) * (8 * split) : n_problems;
   const int var = picp_variant(args->K, args->keep_outliers);

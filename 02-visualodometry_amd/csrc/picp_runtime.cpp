@@ -362,7 +362,6 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
         if (v == 1) split = 1;
         if (v == 2 && grid_of(2) <= b->num_cu) split = 2;
         if (v == 4 && grid_of(4) <= 2 * b->num_cu) split = 4;
-        if (v == 8 && grid_of(8) <= 4 * b->num_cu) split = 8;  // four 256-thread parts per CU (A/B)
         if (b->no_handoff) split = 1;
       }
       // the parts of a split problem wait on each other every round: keep the split only if the
@@ -379,7 +378,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
         b->handoff_grid = grid_of(split);
         b->handoff_resident = res;
         if (grid_of(split) <= res) break;
-        split = (split == 8) ? 4 : (split == 4) ? 2 : 1;
+        split = (split == 4) ? 2 : 1;
       }
       b->split = split;
       if (split > 1) {  // register items per lane for a part

@@ -585,7 +585,7 @@ def test_block_split_matches_oracle(native, oracle, sizes):
     uv = np.concatenate([p["uv"] for p in probs])
     Ti = np.stack([p["T_init"] for p in probs])
     res = {}
-    for split in ("1", "2", "4", "8"):
+    for split in ("1", "2", "4"):
         os.environ["PICP_BLOCK_SPLIT"] = split
         try:
             b = _batch_mode(native, sizes, "block")
