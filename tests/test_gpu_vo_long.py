@@ -10,7 +10,9 @@ segments (a few thousand map rows); this file covers the long form at its full s
   oracle from the GPU's own inputs (the map is append-only, so the GPU's map prefix and its pose of
   frame t are exactly step t's inputs -- teacher forcing, as test_gpu_vo.py):
     - the world match of frame t+1 against the map prefix: n_corr EXACT (bit-exact matcher);
-    - the PICP pose from the GPU's prior: SE(3) log < 1e-4 (north_star);
+    - the PICP pose from the GPU's prior, at the GPU's round count: SE(3) log < 1e-4 (north_star)
+      against the oracle in float64 and in the reference's float32 arithmetic (three summation
+      orders), compared as camera-in-world poses both inverted the way the GPU inverts its own;
     - the points appended after the step: count and descriptors EXACT, positions vs the oracle's
       DLT within 1e-4 relative for 99 % (test_gpu_vo.py's bar).
   and the GPU matcher (picp_match_points, all three forms) is bit-exact against the oracle's
@@ -25,6 +27,8 @@ bounded here; each step is, against the oracle, from the GPU's own inputs.
 """
 import numpy as np
 import pytest
+
+from picp_amd.synth import se3_log_norm
 
 pytestmark = pytest.mark.gpu
 
@@ -48,9 +52,14 @@ def _iso_inverse_f32(T):
     return out
 
 
-def _se3_cw(a, b):
-    from picp_amd.synth import se3_log_norm, rigid_inverse
-    return se3_log_norm(rigid_inverse(np.asarray(a, np.float64)), rigid_inverse(np.asarray(b, np.float64)))
+def _cw_dist(T, P):
+    """SE(3) distance of a solve's world-in-camera result T to the GPU's camera-in-world pose P, in
+    the camera-in-world form the trajectory is kept in: T is inverted exactly as the GPU inverts
+    its own result (_iso_inverse_f32), so both sides are the same function of their solve's output.
+    (Inverting P back instead is not exact: a float32 rotation chained over 1,250 steps is ~5e-5
+    from orthonormal, and R^T or a float64 inverse of P would read that as pose error.)"""
+    from picp_amd.synth import se3_log_norm
+    return se3_log_norm(_iso_inverse_f32(T), P)
 
 
 @pytest.fixture(scope="module")
@@ -95,49 +104,40 @@ def test_vo_8e_segment_teacher_forced_late_steps(oracle, segment_8e, t):
     assert int(wm["accepted"].sum()) == int(R["n_corr"][t + 1])
     pairs = np.stack([np.nonzero(wm["accepted"])[0], wm["best_idx"][wm["accepted"]]], 1).astype(np.int32)
     # the step's prior exactly as the GPU formed it: the float32 inverse of its pose of frame t
-    # (exec/icp_test.cpp:77-78); late in a drifted segment a one-ulp change of the prior moves the
-    # result by ~1e-4, so a prior inverted in float64 and rounded would not be this step's input
+    # (exec/icp_test.cpp:77-78, Isometry3f::inverse: R^T).  Late in the segment P's rotation is
+    # ~5e-5 from orthonormal, so a float64 inverse of P would differ from this prior by ~1e-3 in
+    # translation and would not be this step's input.
     T0 = _iso_inverse_f32(P[t])
     img = uv[off[nf]:off[nf + 1]]
-    T, st = oracle.solve(T0, K, 480, 640, mx[:m], img, pairs, THR)
-    err = _se3_cw(np.linalg.inv(T.astype(np.float64)), P[t + 1])
     gr = int(R["rounds"][t + 1])
     # The icp_test convergence test (relative chi change < 1e-5, exec/icp_test.cpp:99-106) fires at
     # the float noise floor, where the GPU's tree-ordered sums and the oracle's sequential ones
     # differ in the last bits: the two may stop a few rounds apart (as in the C4 converged test).
-    # The round count is then teacher-forced too: the oracle runs exactly the GPU's rounds.
-    Tr, str_ = oracle.solve(T0, K, 480, 640, mx[:m], img, pairs, THR, max_rounds=gr, conv_eps=-1.0)
-    Tf, sf = oracle.solve(T0, K, 480, 640, mx[:m], img, pairs, THR, max_rounds=gr, conv_eps=-1.0,
-                          mode=oracle.MODE_FAITHFUL)
-    err_r = _se3_cw(np.linalg.inv(Tr.astype(np.float64)), P[t + 1])
-    # The step's own sensitivity to float32 rounding: the same solve (same inputs, the GPU's round
-    # count) in the reference's float32 arithmetic (FAITHFUL: sequential float sums, float LDL^T)
-    # with the correspondences summed in their order, in reverse and in a seeded random order, and
-    # in float64 accumulation.  Every one of them is a correct restatement; their spread is what
-    # float rounding alone does to this step's pose.  Late in a drifted segment the map is
-    # inconsistent (chi_in ~ 3.5e5 over ~1,450 inliers: ~15 px residuals), b is a sum of large
-    # cancelling terms and the GN rounds amplify rounding (tools/r05/step_sensitivity.py): the
-    # cloud reaches 1e-4..1e-3 there.  The GPU (float32, tree-ordered sums) is held to 1e-4 or, on
-    # such a step, to 3x the cloud's diameter.
-    rng = np.random.default_rng(t)
-    variants = {"f64": Tr, "faithful": Tf}
-    for name, perm in (("faithful-rev", np.arange(len(pairs))[::-1]), ("faithful-perm", rng.permutation(len(pairs)))):
-        Tv, _ = oracle.solve(T0, K, 480, 640, mx[:m], img, np.ascontiguousarray(pairs[perm]), THR, max_rounds=gr,
-                             conv_eps=-1.0, mode=oracle.MODE_FAITHFUL)
-        variants[name] = Tv
-    cw = {k: np.linalg.inv(v.astype(np.float64)) for k, v in variants.items()}
-    names = list(cw)
-    cloud = max(_se3_cw(cw[a], cw[b]) for i, a in enumerate(names) for b in names[i + 1:])
-    spread = _se3_cw(cw["f64"], cw["faithful"])
-    tol = max(POSE_TOL, 3.0 * cloud)
-    gpu_to = {k: _se3_cw(v, P[t + 1]) for k, v in cw.items()}
-    print("step %d: map %d, n_corr %d, GPU rounds %d (converged %d), oracle free rounds %d; at the GPU's rounds: "
-          "GPU vs %s; oracle cloud diameter %.3g (f64 vs faithful %.3g; tol %.3g); free GPU vs f64 %.3g; chi_in "
-          "GPU %.6g oracle %.6g" % (t, m, len(pairs), gr, int(R["converged"][t + 1]), st["rounds"],
-                                    ", ".join("%s %.3g" % kv for kv in gpu_to.items()), cloud, spread, tol, err,
-                                    float(R["chi_in"][t + 1]), str_["chi_in"]))
-    assert err_r < tol, (t, gpu_to, cloud)
-    assert abs(gr - st["rounds"]) <= 5 or err < tol, (t, gr, st["rounds"], err)
+    # The round count is then teacher-forced too: the oracle runs exactly the GPU's rounds, in
+    # float64 accumulation and in the reference's float32 arithmetic (FAITHFUL: sequential float
+    # sums, float LDL^T) with the correspondences in their order, reversed and in a seeded random
+    # order.  Every one of them is a correct restatement; their spread (the "cloud") is what float
+    # rounding alone does to this step's pose, printed beside the GPU's distance to each.
+    variants = {}
+    for name, mode, order in (("f64", oracle.MODE_F64, None), ("faithful", oracle.MODE_FAITHFUL, None),
+                              ("faithful-rev", oracle.MODE_FAITHFUL, np.arange(len(pairs))[::-1]),
+                              ("faithful-perm", oracle.MODE_FAITHFUL, np.random.default_rng(t).permutation(len(pairs)))):
+        pp = pairs if order is None else np.ascontiguousarray(pairs[order])
+        variants[name], _ = oracle.solve(T0, K, 480, 640, mx[:m], img, pp, THR, max_rounds=gr, conv_eps=-1.0,
+                                         mode=mode)
+    gpu_to = {k: _cw_dist(v, P[t + 1]) for k, v in variants.items()}
+    names = list(variants)
+    cloud = max(se3_log_norm(_iso_inverse_f32(variants[a]), _iso_inverse_f32(variants[b]))
+                for i, a in enumerate(names) for b in names[i + 1:])
+    # the oracle run free (its own convergence test) lands within a few rounds of the GPU's
+    Tfree, st = oracle.solve(T0, K, 480, 640, mx[:m], img, pairs, THR)
+    err_free = _cw_dist(Tfree, P[t + 1])
+    print("step %d: map %d, n_corr %d, GPU rounds %d (converged %d), oracle free rounds %d; at the GPU's rounds GPU "
+          "vs %s; oracle cloud diameter %.3g; free GPU vs f64 %.3g; chi_in GPU %.6g" % (
+              t, m, len(pairs), gr, int(R["converged"][t + 1]), st["rounds"],
+              ", ".join("%s %.3g" % kv for kv in gpu_to.items()), cloud, err_free, float(R["chi_in"][t + 1])))
+    assert max(gpu_to.values()) < POSE_TOL, (t, gpu_to, cloud)
+    assert abs(gr - st["rounds"]) <= 5 or err_free < POSE_TOL, (t, gr, st["rounds"], err_free)
     # the append after step t: add_new_world_points + DLT with (pose t, pose t+1)
     pm = oracle.match_points(desc[off[cf]:off[cf + 1]], dn)
     sel = pm["accepted"].copy()
