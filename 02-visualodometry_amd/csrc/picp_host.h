@@ -15,7 +15,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted, int form, int ksplit,
                                              float4* part);
-extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int form);
+extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form);
 extern "C" int picp_match_prep_kch(int dim);
 
 // records the thread's last error message (picp_last_error) and returns `code`

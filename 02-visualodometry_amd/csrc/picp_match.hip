@@ -278,43 +278,7 @@ __device__ __forceinline__ unsigned mm_shift_in_le(unsigned m, float d, float t)
   return m;
 }
 
-// m = 2m + (v >= 0) for an int v (the sign bit of S' clear): compare into VCC, shift in as carry
-__device__ __forceinline__ unsigned mm_shift_in_ge0(unsigned m, int v) {
-  asm("v_cmp_le_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(m) : "v"(v) : "vcc");
-  return m;
-}
-
-// The 16-element candidate mask of one accumulator (bit 15-i = element i >= 0) as ONE asm block:
-// as 16 separate statements the compiler pads every boundary with an s_nop (it cannot see that a
-// VCC carry chain has no hazard), 16 issue slots per taken block.  The caller has already read
-// every accumulator element (the max tree), so the MFMA result hazard is resolved.
-__device__ __forceinline__ unsigned mm_mask16_ge0(const mm_f16v& acc) {
-  unsigned m = 0;
-  asm("v_cmp_le_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %3\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %4\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %5\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %6\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %7\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %8\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %9\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %10\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %11\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %12\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %13\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %14\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %15\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-      "v_cmp_le_i32 vcc, 0, %16\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
-      : "+v"(m)
-      : "v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]), "v"(acc[4]), "v"(acc[5]), "v"(acc[6]),
-        "v"(acc[7]), "v"(acc[8]), "v"(acc[9]), "v"(acc[10]), "v"(acc[11]), "v"(acc[12]), "v"(acc[13]),
-        "v"(acc[14]), "v"(acc[15])
-      : "vcc");
-  return m;
-}
-
-// The same candidates as mm_mask16_ge0 in 16 instructions instead of 32, laid out by ROW: bit
+// The 16-element candidate mask of one accumulator (element i >= 0) in 16 instructions, by ROW: bit
 // 8k + y is set iff element i = 4k + y is >= 0, and 8k + y = (i & 3) + 8 (i >> 2) is that
 // element's row offset within its 32-row half (the caller adds 32 rb + 4 hf), so a candidate's
 // row is one add from its bit index.  v_perm_b32 selector 9 / 11 turns the sign bit of src1 /
@@ -322,7 +286,7 @@ __device__ __forceinline__ unsigned mm_mask16_ge0(const mm_f16v& acc) {
 // W_y = [neg(4k + y), k = 0..3] as bytes, and three bfi merge bit y of byte k from W_y.  The
 // selectors and masks sit in SGPRs (no VOP3 literals on gfx9; one SGPR per instruction).  The
 // caller has already read every accumulator element (the max tree), so the MFMA result hazard is
-// resolved.  -DMM_MASK_CARRY restores the carry form (A/B builds).
+// resolved.  (A carry chain, compare into VCC + v_addc per element, took 32: round 3.)
 __device__ __forceinline__ unsigned mm_mask16_rows(const mm_f16v& acc) {
   unsigned t, u, v, m;  // W_0 in m, W_y (y > 0) in t, merged as each is done: four temporaries
   asm("v_perm_b32 %[t], %[a4], %[a0], %[s1]\n\t"  // byte 0 = neg(a0), byte 1 = neg(a4)
@@ -348,6 +312,14 @@ __device__ __forceinline__ unsigned mm_mask16_rows(const mm_f16v& acc) {
         [a14] "v"(acc[14]), [a15] "v"(acc[15]), [s1] "s"(0x0C0C0B09u), [s2] "s"(0x05040100u),
         [k1] "s"(0x01010101u), [k3] "s"(0x03030303u), [k7] "s"(0x07070707u), [kf] "s"(0x0F0F0F0Fu));
   return m;
+}
+
+// mm_mask16_rows' row layout (bit 8k + y = element 4k + y) packed to 16 bits, bit i = element i:
+// t = m | m >> 4 puts k = 1 / 3 in the high nibbles of bytes 0 / 2, one v_perm_b32 takes those two
+// bytes
+__device__ __forceinline__ unsigned mm_pack16(unsigned m) {
+  const unsigned t = m | (m >> 4);
+  return __builtin_amdgcn_perm(t, t, 0x0C0C0200u);
 }
 
 // RAD = 1: the accept-only (radius) form for callers that consume only accepted[] and the
@@ -621,18 +593,25 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   }  // pass 1
 
   // ---------------- pass 2: collect the candidates ----------------
-  // Each lane appends its candidates (row, reference) to its OWN list in LDS -- this wave's
-  // s_list words viewed as [64 lanes][LCAP] -- with one plain store each: no atomic and no
-  // register-indexed buffer inside the MFMA loop.  After the pass the wave scatters the entries
-  // into the per-query lists the rescan reads (~2.2 candidates per query on C5, so a lane holds a
-  // few; one that overflows sends every query of its wave to the full scan).  Entries pack the
-  // row (< 64) above a reference index < 2^26 (larger sets take the full scan).
+  // Each lane appends its candidates to its OWN list in LDS -- this wave's s_list words viewed as
+  // [64 lanes][LCAP] -- with one plain store per 32 x 32 block in which it holds any: no atomic, no
+  // per-candidate loop and no register-indexed buffer inside the MFMA loop.  An entry is the
+  // block's 16-element mask (bit i = accumulator element i, row 32 rb + 4 hf + (i & 3) + 8 (i >> 2))
+  // under the block's index (tile << 4 | column block << 1 | rb): the lane's own column r gives
+  // the reference.  After the pass the wave expands the entries into the per-query lists the
+  // rescan reads (~1 candidate per query on C5, so a lane holds a few; a lane that overflows its
+  // list sends every query of its wave to the full scan, as does a range past 4,096 tiles).
   constexpr int LCAP = QPW * MM_CAP / 64;  // RB = 2: 16, RB = 1: 8
+  static_assert(MM_RT / 32 <= 8, "column block index: 3 bits");
   int* const lane_list = &s_list[w][0][0] + lane * LCAP;
   int c_n = 0;
-  auto push = [&](int row, int ref) {
-    if (c_n < LCAP) lane_list[c_n] = (int)(((unsigned)row << 26) | (unsigned)ref);
-    ++c_n;
+  // past LCAP the entry overwrites the last slot and c_n > LCAP sends the wave to the full scan,
+  // so no kept entry is lost
+  auto push_mask = [&](unsigned m16, int64_t t0, int cb, int rb) {
+    if (m16) {
+      lane_list[min(c_n, LCAP - 1)] = (int)((((unsigned)(t0 / MM_RT) << 4 | (unsigned)cb << 1 | (unsigned)rb) << 16) | m16);
+      ++c_n;
+    }
   };
   fetch(0);
   if constexpr (RAD == 2) my_nofold = fold_check(0);
@@ -698,30 +677,11 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #else
             if (__any(mx >= 0)) {  // rare: some lane of the wave holds a candidate
 #endif
-              // the candidate mask in one instruction per element, bit = row offset (the max tree
-              // above has already read every accumulator, so the asm is not the MFMA result's
-              // first reader; the carry form took two per element); a wave vote per element instead (skip the elements no lane has a candidate in)
-              // measured 1.6x slower: 16 uniform branches, and 140 VGPRs cost a wave per SIMD
-#ifdef MM_MASK_CARRY
-              unsigned m = mm_mask16_ge0(acc);
-              while (m) {
-                const int i = 15 - __builtin_ctz(m);
-                m &= m - 1;
-                push(32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf, (int)(t0 + col));
-              }
-#else
-              unsigned m = mm_mask16_rows(acc);  // bit = the element's row offset
-              // push() with the row offset added into the packed entry, and no branch on a full
-              // list: past LCAP the entry overwrites the last slot, and c_n > LCAP then sends the
-              // wave's queries to the full scan (the scatter below), so no kept entry is lost
-              const unsigned pbase = ((unsigned)(32 * rb + 4 * hf) << 26) | (unsigned)(t0 + col);
-              while (m) {
-                const unsigned off = (unsigned)__builtin_ctz(m);
-                m &= m - 1;
-                lane_list[min(c_n, LCAP - 1)] = (int)(pbase + (off << 26));
-                ++c_n;
-              }
-#endif
+              // the candidate mask in one instruction per element (the max tree above has already
+              // read every accumulator, so the asm is not the MFMA result's first reader), packed to
+              // 16 bits; a wave vote per element instead (skip the elements no lane has a candidate
+              // in) measured 1.6x slower: 16 uniform branches, and 140 VGPRs cost a wave per SIMD
+              push_mask(mm_pack16(mm_mask16_rows(acc)), t0, sg + kb, rb);
             }
           }
         }
@@ -749,11 +709,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           m = mm_shift_in_le(m, fmaf(-2.0f, acc[i], n2), RAD == 2 ? radius_tau(rb, i) : tau[rb][i]);
-        while (m) {  // rare: the few candidates of this lane's 16 rows (bit 15-i = element i)
-          const int i = 15 - __builtin_ctz(m);
-          m &= m - 1;
-          push(32 * rb + (i & 3) + 8 * (i >> 2) + 4 * hf, (int)(t0 + col));
-        }
+        push_mask(__builtin_bitreverse32(m) >> 16, t0, sub, rb);  // bit 15-i = element i -> bit i
       }
     }
     if (more) {
@@ -761,24 +717,32 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       stash(buf ^ 1);
     }
   }
-  // scatter the lane lists into the per-query lists (the same LDS words): every entry of the wave
+  // expand the lane lists into the per-query lists (the same LDS words): every entry of the wave
   // is read into registers and the reads have completed before the first write
   {
     const int ln = min(c_n, LCAP);
     unsigned ent[LCAP];
 #pragma unroll
     for (int u = 0; u < LCAP; ++u) ent[u] = (u < ln) ? (unsigned)lane_list[u] : 0u;
-    const bool ovf = __any(c_n > LCAP) || P.nr >= ((int64_t)1 << 26);
+    const bool ovf = __any(c_n > LCAP) || nr_all > ((int64_t)MM_RT << 12);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int u = 0; u < LCAP; ++u)
       if (u < ln) {
-        const int row = (int)(ent[u] >> 26);
-        const int slot = atomicAdd(&s_cnt[w][row], 1);
-        if (slot < MM_CAP) s_list[w][row][slot] = (int)(ent[u] & 0x3ffffffu);
+        const unsigned blk = ent[u] >> 16;
+        const int ref = (int)(blk >> 4) * MM_RT + (int)((blk >> 1) & 7u) * 32 + r;
+        const int rbase = 32 * (int)(blk & 1u) + 4 * hf;
+        unsigned m = ent[u] & 0xffffu;
+        while (m) {
+          const int i = __builtin_ctz(m);
+          m &= m - 1;
+          const int row = rbase + (i & 3) + 8 * (i >> 2);
+          const int slot = atomicAdd(&s_cnt[w][row], 1);
+          if (slot < MM_CAP) s_list[w][row][slot] = ref;
+        }
       }
-    // a dropped entry (full lane list) or a reference index past the packing: the full scan
+    // a dropped entry (full lane list) or a reference range past the packing: the full scan
     if (ovf && lane < QPW) s_cnt[w][lane] = MM_CAP + 1;
   }
   __syncthreads();
@@ -984,7 +948,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
 // PICP_MATCH_KSPLIT=n forces n (1: no split; A/B).  Small problem counts against large reference
 // sets (the VO world match of a few long segments: 8 x 2,000 queries x ~1.9e5 map points) would
 // otherwise run one block per CU or fewer.
-extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int form) {
+extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form) {
   if (form & 2) return 1;  // the exact scan is not split
   static int num_cu = 0;
   if (!num_cu) {
@@ -996,6 +960,9 @@ extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int form) {
   const int64_t base = (int64_t)n_problems * ((max_nq + 32 * MM_WAVES - 1) / (32 * MM_WAVES));
   int64_t k = (4 * (int64_t)num_cu + base - 1) / std::max<int64_t>(base, 1);
   if (const char* e = getenv("PICP_MATCH_KSPLIT")) k = atoi(e);
+  // a range's candidate entries index at most 4,096 tiles (2^20 references; larger ranges take the
+  // full scan): split the largest set at least that far
+  k = std::max<int64_t>(k, (max_nr + ((int64_t)MM_RT << 12) - 1) / ((int64_t)MM_RT << 12));
   return (int)std::max<int64_t>(1, std::min<int64_t>(k, MM_KSPLIT_MAX));
 }
 

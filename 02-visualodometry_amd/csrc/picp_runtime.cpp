@@ -1506,7 +1506,9 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   const size_t n2a = (size_t)std::max<int64_t>(n2, 1);
   const size_t b_prep = ((size_t)n1 + n2a) * (dp * sizeof(_Float16) + 2 * sizeof(float));
   // the reference-range split's scratch (picp_match_ksplit: few problems against many references)
-  const int ks = picp_match_ksplit(n_problems, max_nq, form);
+  int64_t max_nr = 0;
+  for (const MatchProblem& q : probs) max_nr = std::max(max_nr, q.nr);
+  const int ks = picp_match_ksplit(n_problems, max_nq, max_nr, form);
   const size_t b_part = ks > 1 ? (size_t)ks * n_problems * max_nq * sizeof(float4) : 0;
   char* buf = nullptr;
   HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + b_part + 512));

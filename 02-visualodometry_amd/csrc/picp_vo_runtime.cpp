@@ -353,6 +353,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   std::vector<char> is_curr((size_t)h->n_frames, 0);
   int64_t map_slots = 0, n_slots = 0;
   int max_steps = 0;
+  int64_t max_map = 0;  // the largest segment map (the world match's reference set)
   for (int s = 0; s < n_seg; ++s) {
     VoSegment& G = segs[s];
     G.f0 = first[s];
@@ -363,6 +364,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     int64_t cap = frame_n(h, G.f0);  // bootstrap adds <= |frame f0|, step t adds <= |frame f0+t|
     for (int t = 0; t < G.steps; ++t) cap += frame_n(h, G.f0 + t);
     map_slots += std::max<int64_t>(cap, 1);
+    max_map = std::max(max_map, cap);
     n_slots += G.steps + 1;
     max_steps = std::max(max_steps, (int)G.steps);
     for (int64_t f = G.f0; f < G.f0 + G.steps; ++f) is_curr[f] = 1;
@@ -416,7 +418,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   std::vector<Part> p_partw;
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
-    ks_w[c] = picp_match_ksplit(nsc, h->max_obs, h->accept_only);
+    ks_w[c] = picp_match_ksplit(nsc, h->max_obs, max_map, h->accept_only);
     p_partw.push_back(part(ks_w[c] > 1 ? (size_t)ks_w[c] * nsc * h->max_obs * sizeof(float4) : 0));
   }
   size_t part_p_bytes = 0;
@@ -424,7 +426,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     auto need = [&](size_t np) {
       for (size_t q = 0; q < np; q += VO_MAX_GRID_Y) {
         const int n = (int)std::min<size_t>(VO_MAX_GRID_Y, np - q);
-        const int k = picp_match_ksplit(n, h->max_obs, h->accept_only);
+        const int k = picp_match_ksplit(n, h->max_obs, h->max_obs, h->accept_only);
         if (k > 1) part_p_bytes = std::max(part_p_bytes, (size_t)k * n * h->max_obs * sizeof(float4));
       }
     };
@@ -523,7 +525,7 @@ static hipError_t vo_frame_match(picp_vo* h, hipStream_t st, size_t p0, size_t p
   hipError_t e = hipSuccess;
   for (; p0 < p1 && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
     const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - p0);
-    const int ks = h->part_p ? picp_match_ksplit(np, h->max_obs, h->accept_only) : 1;
+    const int ks = h->part_p ? picp_match_ksplit(np, h->max_obs, h->max_obs, h->accept_only) : 1;
     e = picp_launch_match_mfma(st, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1, h->obs_h,
                                h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
                                h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only, ks, h->part_p);

@@ -13,5 +13,5 @@ fi
 : > $OUT/ab.log
 for rep in $(seq ${REPS:-3}); do for W in ${WLS:-c2 c3 c4 c5}; do for v in ${LIBS:-libpicp_amd_base libpicp_amd}; do
   PICP_LIB=$L/$v.so timeout -k 10 200 python bench.py --workload $W --no-cpu --skip-extras --steps ${STEPS:-20} ${ARGS} > $OUT/run.log 2>&1 || { echo "bench $v $W failed"; tail $OUT/run.log; exit 1; }
-  python -c "import json; d=json.loads(open('$OUT/run.log').read().strip().splitlines()[-1]); r=d.get('roofline',{}); print('$W', '$v', d['value'], r.get('kernel_us'), d.get('pose_err_vs_gt_se3', d.get('pose_err_vs_gt_se3_max')))" | tee -a $OUT/ab.log
+  python -c "import json; d=json.loads(open('$OUT/run.log').read().strip().splitlines()[-1]); r=d.get('roofline') or {}; print('$W', '$v', d['value'], r.get('kernel_us'), d.get('pose_err_vs_gt_se3', d.get('pose_err_vs_gt_se3_max')))" | tee -a $OUT/ab.log
 done; done; done
