@@ -15,6 +15,9 @@
 
 #define PICP_BLOCK 256            // threads per linearize block (4 waves of 64)
 #define PICP_NPART 32             // floats per block partial (31 used)
+// persistent mode: pose granule sets per problem -- solver g (g < 8) publishes an L2-kept copy
+// (set 2g) and an agent-scope copy (set 2g + 1), 16 granules (one 128-B line) each
+#define PICP_POSE_SETS 16
 // partial slot layout
 #define PICP_P_H 0                // 21 upper-triangle entries of H (row-major upper)
 #define PICP_P_B 21               // 6 entries of b

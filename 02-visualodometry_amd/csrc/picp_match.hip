@@ -650,7 +650,6 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
         for (int q = 0; q < NQB; ++q) {
           const int kb = q / RB, rb = q - kb * RB;
-          const int col = (sg + kb) * 32 + r;
 #ifdef MM_PIPE
           if (q + 1 < NQB)
             accs[(q + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[(q + 1) % RB], bt[(q + 1) / RB],

@@ -8,11 +8,13 @@
 //   1. every block linearizes its slice at the current pose and publishes its 32-float partial
 //      as 32 granules {tag = round+1, value} (8-byte relaxed agent-scope atomic stores: the R2
 //      hand-off of cdna_hip_programming.md Guideline 16 -- the data IS the flag, no fences);
-//   2. the problem's leader block (its first block) sweeps those granules until every tag
-//      matches, sums them in a FIXED order (deterministic), solves the damped 6x6 system and
-//      applies the update (picp_device.h: finish_round), then publishes the new pose as 16
-//      granules {round+1, word};
-//   3. every other block polls the 16 pose granules (one wave), then starts the next round.
+//   2. the problem's solver blocks (its first PICP_PSOLVERS blocks, one per XCD under round-robin
+//      placement) each sweep those granules until every tag matches, sum them in a FIXED order
+//      (deterministic: every solver gets the same bits), solve the damped 6x6 system and apply
+//      the update (picp_device.h: finish_round), then publish the new pose as 16 granules
+//      {round+1, word} twice: kept in their XCD's L2 and agent-scope;
+//   3. every other block polls its solver's 16 pose granules (one wave) -- the L2 copy once the
+//      first round has shown that it runs on the solver's XCD -- then starts the next round.
 // Correctness does not depend on placement or timing: only tags are trusted.  Blocks must be
 // co-resident (the host caps the grid at the CU count with ~110 VGPRs / 10 KB LDS per block),
 // every spin is bounded by a per-round s_memrealtime deadline (timeout -> error word, loop exits), and
@@ -42,7 +44,16 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #ifndef PICP_POSE_NPOLL  // polls in flight in the followers' pose wait (2 or 3), when staggered
 #define PICP_POSE_NPOLL 2
 #endif
-#define PICP_POSE_GRAN 16   // pose granules per problem: R(9) t(3) done(1) pad(3)
+#define PICP_POSE_GRAN 16   // pose granules per set: R(9) t(3) done(1) solver XCC id(1) pad(2)
+// Solver blocks per problem (-DPICP_PSOLVERS=1 for A/B: one leader, every follower polling its
+// agent-scope pose).  Blocks kb and kb + 8j share an XCD under round-robin placement, so solver
+// kb & 7 publishes where its followers' polls are L2 hits instead of fabric round trips: an
+// agent-scope (sc1) store drops its line from the writer's L2 (MI355X_MICROARCH.md), a
+// workgroup-scope (sc0) store keeps it there.  Placement is not guaranteed, so the solver also
+// publishes agent-scope and carries its XCC id; a follower on another XCD polls that copy.
+#ifndef PICP_PSOLVERS
+#define PICP_PSOLVERS 8
+#endif
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
 // never hoisted out of a spin loop)
 #define PICP_AUX_SC1_VOLATILE ((int)(16u | 0x80000000u))
@@ -104,6 +115,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   __shared__ float s_pose[12];
   __shared__ int s_done;
   __shared__ int s_tmo;  // a wait of this block timed out (the error word is for the host)
+  __shared__ int s_l2;   // a follower on its solver's XCD: poll the L2 copy of the pose
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nblk = A.nblk_u;
@@ -112,13 +124,19 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   const int first = kb * A.ipb;
   const int count = max(0, min(A.ipb, A.n_u - first));
   const int64_t base = (int64_t)p * A.stride_u + first;
-  const bool leader = (kb == 0);
+  const bool leader = (kb == 0);                 // keeps the loop state and the tag base
+  const bool solver = (kb < PICP_PSOLVERS);      // sweeps, solves and publishes the pose
+  const int sg = kb % PICP_PSOLVERS;             // this block's solver
   // partial granules are double-buffered by round parity, so correctness does not rest on the
   // leader having swept round r before any block publishes round r+1
   const size_t part_stride = (size_t)gridDim.x * PICP_NPART;
   gu64_t* my_part0 = ((gu64_t*)gpart) + (size_t)blockIdx.x * PICP_NPART;
   gu64_t* prob_part0 = ((gu64_t*)gpart) + (size_t)p * nblk * PICP_NPART;
-  gu64_t* prob_pose = ((gu64_t*)gpose) + (size_t)p * PICP_POSE_GRAN;
+  gu64_t* prob_pose = ((gu64_t*)gpose) + (size_t)p * PICP_POSE_SETS * PICP_POSE_GRAN;
+  gu64_t* pose_l2 = prob_pose + (size_t)(2 * sg) * PICP_POSE_GRAN;      // kept in the XCD's L2
+  gu64_t* pose_gl = prob_pose + (size_t)(2 * sg + 1) * PICP_POSE_GRAN;  // agent scope
+  unsigned my_xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
   gu32_t* errw = ((gu32_t*)err);
   // Granule tags are tbase + round.  tbase is the problem's count of rounds run by every earlier
   // launch on these buffers (its leader advances it after the last round), so tags never repeat
@@ -154,6 +172,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
     for (int i = 0; i < 3; ++i) s_pose[9 + i] = s.t[i];
     s_done = s.done;
     s_tmo = 0;
+    s_l2 = 0;
     if (leader && s.done) st_out[p] = s;
   }
   __syncthreads();
@@ -224,7 +243,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
     }
     PSTAMP(1);
 
-    if (leader) {
+    if (solver) {
       // ---- 2. sweep the problem's partials: 16-B sc1 loads of granule pairs (2c, 2c+1) of
       //         blocks g + NG*i (c = tid&15, g = tid>>4); each 8-B half carries its own tag ----
       const int c = tid & 15, g = tid >> 4;
@@ -327,14 +346,20 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
 #pragma unroll
           for (int i = 0; i < 3; ++i) w = (lane == 9 + i) ? pt[i] : w;
           w = (lane == 12) ? __int_as_float(o.done) : w;
-          if (lane < PICP_POSE_GRAN) __hip_atomic_store(prob_pose + lane, granule(tbase + epoch, w), RLX_AGENT);
+          w = (lane == 13) ? __uint_as_float(my_xcc) : w;
+          if (lane < PICP_POSE_GRAN) {
+            const unsigned long long gw = granule(tbase + epoch, w);
+            if (PICP_PSOLVERS > 1)
+              __hip_atomic_store(pose_l2 + lane, gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(pose_gl + lane, gw, RLX_AGENT);
+          }
           if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < 9; ++i) s_pose[i] = pr[i];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) s_pose[9 + i] = pt[i];
+            for (int i = 0; i < 3; ++i) s_pose[9 + i] = pt[i];
             s_done = o.done;
-            if (o.done) {
+            if (o.done && leader) {
               store_state(st_out + p, pr, pt, chi_prev, o, (int)epoch);
               // every block of the problem read tbase before publishing round 1, and this is
               // after its last round: the next launch's tags start past this one's
@@ -358,7 +383,9 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         // exit keeps its registers until the next round's wait consumes them (pose_sink), so
         // nothing waits on it.
         const int gl = lane < PICP_POSE_GRAN ? lane : PICP_POSE_GRAN - 1;
-        auto poll = [&]() -> unsigned long long { return __hip_atomic_load(prob_pose + gl, RLX_AGENT); };
+        // sc1 loads either way: past the L1, served by the L2 (the L2 copy's line stays there)
+        const gu64_t* src = (PICP_PSOLVERS > 1 && s_l2) ? pose_l2 : pose_gl;
+        auto poll = [&]() -> unsigned long long { return __hip_atomic_load(src + gl, RLX_AGENT); };
         auto good = [&](unsigned long long v) { return __all((unsigned)(v >> 32) == tbase + epoch); };
         pose_sink ^= pa ^ pb ^ pc;  // last round's polls: long complete
         bool tmo = false;
@@ -391,10 +418,11 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           if (lane < 12) gp = __float_as_uint(s_pose[lane]);
         }
 #else
+        const gu64_t* src = (PICP_PSOLVERS > 1 && s_l2) ? pose_l2 : pose_gl;
         for (;;) {
           bool ok = true;
           if (lane < PICP_POSE_GRAN) {
-            gp = __hip_atomic_load(prob_pose + lane, RLX_AGENT);
+            gp = __hip_atomic_load(src + lane, RLX_AGENT);
             ok = (unsigned)(gp >> 32) == tbase + epoch;
           }
           if (__all(ok)) break;
@@ -409,6 +437,8 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
 #endif
         if (lane < 12) s_pose[lane] = __uint_as_float((unsigned)gp);
         if (lane == 12) s_done = (int)(unsigned)gp;
+        // the solver's XCC id: from the next round on, poll the L2 copy when it is this XCD's
+        if (PICP_PSOLVERS > 1 && lane == 13) s_l2 = ((unsigned)gp == my_xcc) ? 1 : 0;
       }
       __syncthreads();
       PSTAMP(2);

@@ -452,12 +452,12 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
     b->np_cap = np;
   }
   if (uses_err_word(b)) {
-    // persistent: error word | pose granules | partial granules (x2 parities);
+    // persistent: error word (128-B line) | pose granule sets | partial granules (x2 parities);
     // split block: error word | exchange granules (x2 parities, 64 per block and problem held)
     // | tag bases
     const int64_t sgrid = xg_grid(b);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
-                        ? (size_t)round_up(16 + (int64_t)np * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
+                        ? (size_t)round_up(128 + (int64_t)np * PICP_POSE_SETS * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
                                                (int64_t)np * 4, 256)
                         : (size_t)round_up(16 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
     if (b->sync_bytes > b->sync_cap) {
@@ -598,8 +598,10 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
     // no memset per launch: granule tags continue from the per-problem tag bases the previous
     // launch left (picp_persistent.hip), so nothing a previous launch wrote can match
     unsigned int* err = reinterpret_cast<unsigned int*>(b->sync);
-    unsigned long long* gpose = reinterpret_cast<unsigned long long*>(b->sync + 16);
-    unsigned long long* gpart = gpose + (size_t)b->np * PICP_POSE_GRAN;
+    // pose sets on 128-B lines of their own (an agent-scope store to a line drops it from the
+    // XCD's L2, so an L2-kept set must not share a line with anything stored agent-scope)
+    unsigned long long* gpose = reinterpret_cast<unsigned long long*>(b->sync + 128);
+    unsigned long long* gpart = gpose + (size_t)b->np * PICP_POSE_SETS * PICP_POSE_GRAN;
     unsigned int* tagbase = reinterpret_cast<unsigned int*>(gpart + 2 * (size_t)b->nblk * PICP_NPART);
     return picp_launch_persistent(b->stream, b->nblk, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(),
                                   &b->args, b->init_d, b->st_d[0], gpart, gpose, err, tagbase,
