@@ -453,13 +453,13 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
   }
   if (uses_err_word(b)) {
     // persistent: error word (128-B line) | pose granule sets | partial granules (x2 parities);
-    // split block: error word | exchange granules (x2 parities, 64 per block and problem held)
-    // | tag bases
+    // split block: error word (128-B line) | exchange granules (x2 parities, 64 per block and
+    // problem held) | tag bases
     const int64_t sgrid = xg_grid(b);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
                         ? (size_t)round_up(128 + (int64_t)np * PICP_POSE_SETS * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
                                                (int64_t)np * 4, 256)
-                        : (size_t)round_up(16 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
+                        : (size_t)round_up(128 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
       b->sync = nullptr;
@@ -587,7 +587,9 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
     if (b->split > 1) {  // tags continue from the per-slot tag bases: no memset per launch
       const int64_t sgrid = xg_grid(b);
       err = reinterpret_cast<unsigned int*>(b->sync);
-      xg = reinterpret_cast<unsigned long long*>(b->sync + 16);
+      // every block's 512-B granule set on whole 128-B lines: at sync + 16 each set shared a line
+      // with its neighbour's, and C4 at 128 frames ran 3.5 % slower (profiles/r05/xg_align/)
+      xg = reinterpret_cast<unsigned long long*>(b->sync + 128);
       tagbase = reinterpret_cast<unsigned int*>(xg + 2 * sgrid * 64);
     }
     return picp_launch_block(b->stream, b->np, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(), &b->args,
