@@ -43,14 +43,20 @@ def main():
         rel = (st - t0) * 10
         print("round %d (%d blocks), ns from first round start" % (11 + r, nb))
         print("  leader: start %d published %d swept(all threads) %d combined %d solve_start %d solve_end %d" % (rel[0,0], rel[0,1], rel[0,2], rel[0,3], rel[0,4], rel[0,5]))
-        others = rel[1:]
+        # blocks 1..7 are the other solvers (picp_persistent.hip PICP_PSOLVERS), the rest followers
+        ns = min(8, nb)
+        if ns > 1:
+            sol = rel[1:ns]
+            print("  solvers 1-%d: published median %d, swept median %d (max %d), solve_end median %d (max %d)" % (
+                ns - 1, np.median(sol[:, 1]), np.median(sol[:, 2]), sol[:, 2].max(), np.median(sol[:, 5]), sol[:, 5].max()))
+        others = rel[ns:] if nb > ns else rel[1:]
         for k, nm in enumerate(["start", "published", "pose_received"]):
-            print("  others %-14s median %6d  min %6d  max %6d" % (nm, np.median(others[:, k]), others[:, k].min(), others[:, k].max()))
+            print("  followers %-11s median %6d  min %6d  max %6d" % (nm, np.median(others[:, k]), others[:, k].min(), others[:, k].max()))
+        last_pub = int(rel[:, 1].max())
         # the leader's sweep passes (thread 0): issue -> loads returned, ns from the round start
         p = sw[r].astype(np.int64)
         n = int(np.count_nonzero(p)) // 2
         passes = [((p[2 * i] - t0) * 10, (p[2 * i + 1] - t0) * 10) for i in range(n)]
-        last_pub = int(others[:, 1].max())
         print("  leader sweep passes (issue..return ns): %s" % "  ".join("%d..%d" % x for x in passes))
         if passes:
             dur = [b - a for a, b in passes]
