@@ -14,14 +14,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const struct MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted, int form, int ksplit,
-                                             float4* part, const struct MatchOrder* ord = nullptr);
-// the key order of the window form (struct MatchOrder): the sets (q_off, nq) (side 0) or
-// (r_off, nr) (side 1) of n_sets problems, each of at most picp_match_order_max() descriptors
-extern "C" hipError_t picp_launch_match_order(hipStream_t stream, const struct MatchProblem* sets, int n_sets,
-                                              int side, const float* desc, int dim, const _Float16* h,
-                                              const float* n1, const float* n2, int32_t* perm, float* key,
-                                              _Float16* hs, float* n1s, float* n2s);
-extern "C" int64_t picp_match_order_max(void);
+                                             float4* part);
 extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form);
 extern "C" int picp_match_prep_kch(int dim);
 

@@ -100,21 +100,6 @@ struct MatchProblem {
   int64_t q_off, nq, r_off, nr;
 };
 
-// The matcher's key-ordered window form (picp_match.hip, picp_launch_match_order): every
-// problem's queries and references ordered by their first component.  perm: slot -> index within
-// the problem; key: that component in slot order (+inf where it is not finite); r_h / r_n1 / r_n2:
-// the references' prep rows and norms in slot order.  All indexed like the prep arrays (q_off /
-// r_off + slot).
-struct MatchOrder {
-  const int32_t* q_perm;
-  const float* q_key;
-  const int32_t* r_perm;
-  const float* r_key;
-  const _Float16* r_h;
-  const float* r_n1;
-  const float* r_n2;
-};
-
 // ---------------------------------------------------------------------------------------
 // essential-matrix bootstrap (picp_essential.hip; src/cam.cpp:37-91), by value
 struct EssArgs {

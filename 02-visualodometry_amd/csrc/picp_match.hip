@@ -335,15 +335,7 @@ __device__ __forceinline__ unsigned mm_pack16(unsigned m) {
 #ifndef MM_MINB
 #define MM_MINB 1
 #endif
-// WIN = 1 (RAD = 2 only): the key-ordered window form (struct MatchOrder, picp_launch_match_order).
-// Queries and references are visited in the order of their first component; a block's queries
-// span keys [k_lo, k_hi] and it scans only the reference tiles whose keys meet
-// [k_lo - w, k_hi + w], w = 1.001 sqrt(R).  Exact: a reference outside has |q0 - r0| > w for every
-// query of the block, and the reference's distance, an in-order FP32 sum of non-negative terms,
-// is at least its first term fl(fl(q0 - r0)^2) > R, so it is no candidate of the radius form.
-// Candidates are reference slots, mapped to indices through r_perm before the rescan, whose
-// update is visiting-order-independent; outputs go to the queries' own indices (q_perm).
-template <int KCH, int RAD, int RB, int WIN>
+template <int KCH, int RAD, int RB>
 __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
@@ -351,8 +343,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const MatchProblem* __restrict__ probs, int dim, float dist_thr, float ratio_thr,
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
     float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
-    int xcd_map, int ksplit, float4* __restrict__ part, int64_t part_nq, MatchOrder ord) {
-  static_assert(!WIN || RAD == 2, "the window form is the folded radius form's");
+    int xcd_map, int ksplit, float4* __restrict__ part, int64_t part_nq) {
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
@@ -399,9 +390,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     ks = blockIdx.x / gx;
   }
   MatchProblem P = probs[pid];
-  const int64_t r_off0 = P.r_off;  // the problem's references (WIN: P.r_off moves to the window)
   int64_t r_lo = 0;  // this block's references: [r_lo, r_lo + P.nr) of the problem's (P is local)
-  if (!WIN && ksplit > 1) {
+  if (ksplit > 1) {
     const int64_t kc = mm_kchunk(P.nr, ksplit);
     r_lo = (int64_t)ks * kc;
     if (r_lo >= P.nr) return;  // an empty range (the merge reads only mm_nsplit ranges)
@@ -411,41 +401,12 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   const int64_t q0 = (int64_t)qblk * QPB;
   if (q0 >= P.nq) return;  // whole block past this problem
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
-  const int64_t qw = q0 + (int64_t)w * QPW;  // this wave's first query (WIN: query slot)
-  // WIN: the query index of slot s (problem-relative)
-  auto qidx = [&](int64_t s) -> int64_t { return WIN ? (int64_t)ord.q_perm[P.q_off + s] : s; };
-  if constexpr (WIN) {
-    // the block's reference window, in whole 32-row column blocks [ca, cb): one is outside iff its
-    // last key is below k_lo - w or its first key above k_hi + w (keys ascend); counted over the
-    // block.  The window's tiles start at its first row (a partial last tile, as at a set's end).
-    const double wd = sqrt((double)mm_radius(dist_thr, ratio_thr)) * 1.001;
-    const double lo = (double)ord.q_key[P.q_off + q0] - wd;
-    const double hi = (double)ord.q_key[P.q_off + min(q0 + QPB, P.nq) - 1] + wd;
-    const int64_t nr = P.nr, C = (nr + 31) / 32;
-    int64_t below = 0, above = 0;
-    for (int64_t cc = 0; cc < C; cc += MM_BLOCK) {
-      const int64_t c = cc + tid;
-      bool b = false, a = false;
-      if (c < C) {
-        b = (double)ord.r_key[r_off0 + min(c * 32 + 31, nr - 1)] < lo;
-        a = (double)ord.r_key[r_off0 + c * 32] > hi;
-      }
-      below += __syncthreads_count(b);
-      above += __syncthreads_count(a);
-    }
-    // this block's share of the window (ksplit > 1: the ks-th of ksplit ranges of whole tiles,
-    // maybe empty)
-    const int64_t wa = below * 32, wb = max(wa, min((C - above) * 32, nr));
-    const int64_t cs = ((wb - wa + ksplit - 1) / ksplit + MM_RT - 1) / MM_RT * MM_RT;
-    r_lo = min(wa + (int64_t)ks * cs, wb);
-    P.r_off = r_off0 + r_lo;  // the tile fetch reads the slot-ordered prep (ord.r_h, passed as r_h)
-    P.nr = min(r_lo + cs, wb) - r_lo;
-  }
+  const int64_t qw = q0 + (int64_t)w * QPW;  // this wave's first query
 
   mm_half8 qa[RB][KCH];  // A operands: query qw + 32 rb + r, halves [16c + 8 hf, +8)
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
-    const int64_t qi = qidx(min(qw + 32 * rb + r, P.nq - 1));
+    const int64_t qi = min(qw + 32 * rb + r, P.nq - 1);
 #pragma unroll
     for (int c = 0; c < KCH; ++c) {
       qa[rb][c] = *reinterpret_cast<const mm_half8*>(q_h + (P.q_off + qi) * DP + 16 * c + 8 * hf);
@@ -456,7 +417,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   }
   if (lane < QPW) {
     const int64_t qi = qw + lane;
-    float nq = (qi < P.nq) ? q_n1[P.q_off + qidx(qi)] : 0.0f;  // +inf: unsafe query
+    float nq = (qi < P.nq) ? q_n1[P.q_off + qi] : 0.0f;  // +inf: unsafe query
     if (RAD == 2 && !(nq <= MM_FOLD_MAX)) nq = INFINITY;  // outside the fold's range: full scan
     s_nq[w][lane] = nq;
     s_cnt[w][lane] = 0;
@@ -652,11 +613,9 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       ++c_n;
     }
   };
-  if (nr_all > 0) {  // (WIN: a block's window may be empty)
-    fetch(0);
-    if constexpr (RAD == 2) my_nofold = fold_check(0);
-    stash(0);
-  }
+  fetch(0);
+  if constexpr (RAD == 2) my_nofold = fold_check(0);
+  stash(0);
   buf = 0;
   for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
     bool fold = false;
@@ -790,10 +749,9 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   // ---------------- exact update over the candidates, in index order ----------------
   const int64_t qi = qw + lane;
   if (lane < QPW && qi < P.nq) {
-    const int64_t qo = qidx(qi);  // the query's index (WIN: qi is its slot)
     float q[DMAX];
 #pragma unroll
-    for (int k = 0; k < DMAX; ++k) q[k] = (k < dim) ? q_desc[(P.q_off + qo) * dim + k] : 0.0f;
+    for (int k = 0; k < DMAX; ++k) q[k] = (k < dim) ? q_desc[(P.q_off + qi) * dim + k] : 0.0f;
     float best = FLT_MAX, second = FLT_MAX;  // :78-79
     int32_t bi = -1;
 #ifdef MM_DIAG_NORESCAN  // diagnostic timing build only: no exact rescan
@@ -808,22 +766,10 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) atomicAdd(&picp_match_stats[0], 1ull);
 #endif
     if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) {  // slow path: the reference's full scan
-      if constexpr (WIN) {
-        // over the window's slots (the references outside are no candidates), in slot order: the
-        // order-independent update below
-        for (int64_t j = 0; j < P.nr; ++j) {
-          const int32_t o = ord.r_perm[P.r_off + j];
-          const float d = mm_exact_dist(q, r_desc + (r_off0 + o) * dim, dim);
-          if (d < best) { second = best; best = d; bi = o; }
-          else if (d == best) { second = best; bi = min(bi, o); }
-          else if (d < second) second = d;
-        }
-      } else {
-        for (int64_t j = 0; j < P.nr; ++j) {
-          const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
-          if (d < best) { second = best; best = d; bi = (int32_t)j; }
-          else if (d < second) second = d;
-        }
+      for (int64_t j = 0; j < P.nr; ++j) {
+        const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
+        if (d < best) { second = best; best = d; bi = (int32_t)j; }
+        else if (d < second) second = d;
       }
     } else {
       // The candidates in LDS are in no particular order (lanes append them with LDS atomics).
@@ -842,9 +788,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
         for (int u = 0; u < MM_RQ; ++u) {
           jj[u] = (k0 + u < n) ? s_list[w][lane][k0 + u] : -1;
-          if constexpr (WIN)  // slot -> the reference's index
-            if (jj[u] >= 0) jj[u] = ord.r_perm[P.r_off + jj[u]];
-          const float* rp = r_desc + ((WIN ? r_off0 : P.r_off) + max(jj[u], 0)) * dim;
+          const float* rp = r_desc + (P.r_off + max(jj[u], 0)) * dim;
 #pragma unroll
           for (int k = 0; k < DMAX; ++k) rr[u][k] = (jj[u] >= 0 && k < dim) ? rp[k] : 0.0f;
         }
@@ -868,25 +812,22 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
       }
     }
-    if (ksplit > 1)  // this range's top-2 (problem index), merged by picp_match_merge_kernel
-      part[((int64_t)ks * n_problems + pid) * part_nq + qo] =
-          make_float4(__int_as_float(bi >= 0 ? (int32_t)(WIN ? bi : bi + r_lo) : -1), best, second, 0.0f);
+    if (ksplit > 1)  // this range's top-2 (global index), merged in range order by picp_match_merge_kernel
+      part[((int64_t)ks * n_problems + pid) * part_nq + qi] =
+          make_float4(__int_as_float(bi >= 0 ? (int32_t)(bi + r_lo) : -1), best, second, 0.0f);
     else
-      match_store(P, P.q_off + qo, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+      match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
                   accepted);  // :100-103
   }
 }
 
-// The reference ranges of a split launch, merged: the reference's in-order strict-'<' scan over
-// the whole set yields best = the smallest of the ranges' bests (a tie keeps the lower index: the
-// index ranges are disjoint, so the smaller of the two first indices), second = the second
-// smallest of the union.  Each range's (best, first index, second) is exactly its own in-order
-// scan's (index-order-independent update above), so the merged triple is the whole scan's.  All
-// ksplit ranges are read in the window form (all_parts; a block's empty window share writes
-// FLT_MAX, -1), the mm_nsplit non-empty ones otherwise.  One thread per query.
+// The reference ranges of a split launch, merged in index order: the reference's in-order
+// strict-'<' scan over range 0, then range 1, ... yields best = the smaller best (a tie keeps the
+// earlier range's, i.e. the lower index), second = the second smallest of the union.  Each range's
+// (best, first index, second) is exactly its own in-order scan's (index-order-independent update
+// above), so the merged triple is the whole scan's.  One thread per query.
 extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, int n_problems,
-                                                   int ksplit, int all_parts, const float4* __restrict__ part,
-                                                   int64_t part_nq,
+                                                   int ksplit, const float4* __restrict__ part, int64_t part_nq,
                                                    float dist_thr, float ratio_thr, int32_t* __restrict__ best_idx,
                                                    float* __restrict__ best_dist, float* __restrict__ second_dist,
                                                    int32_t* __restrict__ accepted) {
@@ -894,7 +835,7 @@ extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restric
   const MatchProblem P = probs[pid];
   const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (qi >= P.nq) return;
-  const int ns = all_parts ? ksplit : mm_nsplit(P.nr, ksplit);
+  const int ns = mm_nsplit(P.nr, ksplit);
   float best = FLT_MAX, second = FLT_MAX;  // src/my_utilities.h:78-79
   int32_t bi = -1;
   for (int k = 0; k < ns; ++k) {
@@ -905,8 +846,7 @@ extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restric
       best = b;
       bi = __float_as_int(r.x);
     } else if (b == best) {
-      second = best;  // two equal values in the multiset; the lower index stays
-      bi = min(bi, __float_as_int(r.x));  // (both -1 when best is FLT_MAX: never mixed)
+      second = best;  // two equal values in the multiset; the earlier index stays
     } else {
       second = fminf(second, b);
     }
@@ -926,82 +866,6 @@ extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* de
   return hipGetLastError();
 }
 
-// The key order of the window form (struct MatchOrder): one block per set sorts (key, index) pairs
-// in LDS (bitonic, padded to a power of two), key = the first component as an order-preserving
-// integer (non-finite: last), ties by index, then writes perm, key and the prep rows and norms in
-// slot order (hs == nullptr: perm and key only -- a query set, whose rows the matcher reads
-// through perm).  A set larger than MM_ORDER_MAX is left unwritten: the host never orders one
-// (picp_match_order_max).
-#define MM_ORDER_MAX 8192
-#define MM_ORDER_BLOCK 1024
-extern "C" int64_t picp_match_order_max(void) { return MM_ORDER_MAX; }
-extern "C" __global__ __launch_bounds__(MM_ORDER_BLOCK) void picp_match_order_kernel(
-    const MatchProblem* __restrict__ sets, int side, const float* __restrict__ desc, int dim,
-    const _Float16* __restrict__ h, const float* __restrict__ n1, const float* __restrict__ n2, int dp,
-    int32_t* __restrict__ perm, float* __restrict__ key, _Float16* __restrict__ hs, float* __restrict__ n1s,
-    float* __restrict__ n2s) {
-  __shared__ unsigned long long s[MM_ORDER_MAX];
-  const MatchProblem S = sets[blockIdx.x];
-  const int64_t off = side ? S.r_off : S.q_off, n64 = side ? S.nr : S.nq;
-  if (n64 <= 0 || n64 > MM_ORDER_MAX) return;  // (block-uniform)
-  const int n = (int)n64, tid = threadIdx.x;
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int i = tid; i < np2; i += MM_ORDER_BLOCK) {
-    unsigned long long v = ~0ull;
-    if (i < n) {
-      const float x = desc[(off + i) * dim];
-      const unsigned u = __float_as_uint(x);
-      const unsigned k = __builtin_isfinite(x) ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0xFFFFFFFFu;
-      v = ((unsigned long long)k << 32) | (unsigned)i;
-    }
-    s[i] = v;
-  }
-  __syncthreads();
-  for (int k = 2; k <= np2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < np2; i += MM_ORDER_BLOCK) {
-        const int l = i ^ j;
-        if (l > i) {
-          const unsigned long long a = s[i], b = s[l];
-          if ((a > b) == ((i & k) == 0)) {
-            s[i] = b;
-            s[l] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  for (int i = tid; i < n; i += MM_ORDER_BLOCK) {
-    const int src = (int)(unsigned)s[i];
-    const float x = desc[(off + src) * dim];
-    perm[off + i] = src;
-    key[off + i] = __builtin_isfinite(x) ? x : INFINITY;
-    if (hs) {
-      n1s[off + i] = n1[off + src];
-      n2s[off + i] = n2[off + src];
-    }
-  }
-  if (!hs) return;  // (a query set: perm and key only)
-  const int cpr = dp / 8;  // 16-B chunks per prep row
-  for (int c = tid; c < n * cpr; c += MM_ORDER_BLOCK) {
-    const int i = c / cpr, part = c - i * cpr, src = (int)(unsigned)s[i];
-    *reinterpret_cast<mm_half8*>(hs + (off + i) * dp + 8 * part) =
-        *reinterpret_cast<const mm_half8*>(h + (off + src) * dp + 8 * part);
-  }
-}
-
-extern "C" hipError_t picp_launch_match_order(hipStream_t stream, const MatchProblem* sets, int n_sets, int side,
-                                              const float* desc, int dim, const _Float16* h, const float* n1,
-                                              const float* n2, int32_t* perm, float* key, _Float16* hs,
-                                              float* n1s, float* n2s) {
-  if (n_sets <= 0) return hipSuccess;
-  if (dim < 1 || dim > PICP_MATCH_MAXD || n_sets > 2147483647) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(picp_match_order_kernel, dim3((unsigned)n_sets), dim3(MM_ORDER_BLOCK), 0, stream, sets, side,
-                     desc, dim, h, n1, n2, 16 * picp_match_prep_kch(dim), perm, key, hs, n1s, n2s);
-  return hipGetLastError();
-}
-
 // The pre-filtered match over prepped descriptors (picp_launch_match_prep).  form (include/picp_c.h
 // PICP_MATCH_FORM_*): bit 0 = the accept-only radius form (only accepted[] and the best index of
 // accepted queries are defined), bit 1 = the exact scan (the same results as the full form; for
@@ -1013,7 +877,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted, int form, int ksplit,
-                                             float4* part, const MatchOrder* ord) {
+                                             float4* part) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
   if (ksplit < 1 || ksplit > MM_KSPLIT_MAX || (ksplit > 1 && !part)) return hipErrorInvalidValue;
   const bool accept_only = (form & 1) != 0;
@@ -1048,45 +912,30 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   const dim3 g = xcd_map ? dim3((unsigned)(8 * ((ngroups + 7) / 8) * gx))
                          : dim3((unsigned)(gx * ksplit), (unsigned)n_problems);
   const int64_t part_nq = max_nq;
-  // the window form: the folded form over the key-ordered sets (ord), its reference tiles from
-  // the slot-ordered prep
-  const bool win = fold && ord != nullptr;
-  const MatchOrder no{};
-  const MatchOrder& od = win ? *ord : no;
-  if (win) {
-    r_h = ord->r_h;
-    r_n1 = ord->r_n1;
-    r_n2 = ord->r_n2;
-  }
-#define PICP_LAUNCH_MM4(KC, RD, R, W)                                                                        \
-  hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD, R, W>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc,    \
-                     q_h, q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist,         \
-                     second_dist, accepted, n_problems, gx, xcd_map, ksplit, part, part_nq, od)
-#define PICP_LAUNCH_MM3(KC, RD, R) PICP_LAUNCH_MM4(KC, RD, R, 0)
+#define PICP_LAUNCH_MM3(KC, RD, R)                                                                          \
+  hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD, R>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h,  \
+                     q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, \
+                     accepted, n_problems, gx, xcd_map, ksplit, part, part_nq)
 #define PICP_LAUNCH_MM(KC, RD)                   \
   {                                              \
     if (rb == 2) PICP_LAUNCH_MM3(KC, RD, 2);     \
     else PICP_LAUNCH_MM3(KC, RD, 1);             \
   }
   if (dim <= 16) {
-    if (win) {
-      if (rb == 2) PICP_LAUNCH_MM4(1, 2, 2, 1);
-      else PICP_LAUNCH_MM4(1, 2, 1, 1);
-    } else if (fold) PICP_LAUNCH_MM(1, 2)
+    if (fold) PICP_LAUNCH_MM(1, 2)
     else if (rad) PICP_LAUNCH_MM(1, 1)
     else PICP_LAUNCH_MM(1, 0)
   } else {
     if (rad) PICP_LAUNCH_MM(2, 1)
     else PICP_LAUNCH_MM(2, 0)
   }
-#undef PICP_LAUNCH_MM4
 #undef PICP_LAUNCH_MM3
 #undef PICP_LAUNCH_MM
   if (ksplit > 1) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(picp_match_merge_kernel, dim3((unsigned)((max_nq + 255) / 256), (unsigned)n_problems),
-                       dim3(256), 0, stream, probs, n_problems, ksplit, win ? 1 : 0, (const float4*)part, part_nq, dist_thr,
+                       dim3(256), 0, stream, probs, n_problems, ksplit, (const float4*)part, part_nq, dist_thr,
                        ratio_thr, best_idx, best_dist, second_dist, accepted);
   }
   return hipGetLastError();

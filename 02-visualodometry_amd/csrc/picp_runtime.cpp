@@ -1514,14 +1514,8 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   for (const MatchProblem& q : probs) max_nr = std::max(max_nr, q.nr);
   const int ks = picp_match_ksplit(n_problems, max_nq, max_nr, form);
   const size_t b_part = ks > 1 ? (size_t)ks * n_problems * max_nq * sizeof(float4) : 0;
-  // the window form (picp_launch_match_order) of the accept-only form: every set within the
-  // order kernel's size; PICP_MATCH_ORDER=0 turns it off (A/B)
-  const char* oe = getenv("PICP_MATCH_ORDER");
-  const bool order = form == PICP_MATCH_FORM_ACCEPT_ONLY && dim <= 12 && n2 > 0 && !(oe && atoi(oe) == 0) &&
-                     max_nq <= picp_match_order_max() && max_nr <= picp_match_order_max();
-  const size_t b_ord = order ? (size_t)n1 * 8 + n2a * (8 + dp * sizeof(_Float16) + 8) + 64 : 0;
   char* buf = nullptr;
-  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + b_part + b_ord + 512));
+  HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + b_part + 512));
   char* cur = buf;
   auto carve = [&](size_t bytes) { char* r = cur; cur += (bytes + 15) / 16 * 16; return r; };
   MatchProblem* d_probs = (MatchProblem*)carve(b_probs);
@@ -1538,39 +1532,14 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   float* r_n1 = (float*)carve(n2a * 4);
   float* r_n2 = (float*)carve(n2a * 4);
   float4* d_part = ks > 1 ? (float4*)carve(b_part) : nullptr;
-  MatchOrder ord{};
-  int32_t* o_qp = nullptr;
-  float* o_qk = nullptr;
-  int32_t* o_rp = nullptr;
-  float *o_rk = nullptr, *o_rn1 = nullptr, *o_rn2 = nullptr;
-  _Float16* o_rh = nullptr;
-  if (order) {
-    o_qp = (int32_t*)carve((size_t)n1 * 4);
-    o_qk = (float*)carve((size_t)n1 * 4);
-    o_rp = (int32_t*)carve(n2a * 4);
-    o_rk = (float*)carve(n2a * 4);
-    o_rh = (_Float16*)carve(n2a * dp * sizeof(_Float16));
-    o_rn1 = (float*)carve(n2a * 4);
-    o_rn2 = (float*)carve(n2a * 4);
-    ord = MatchOrder{o_qp, o_qk, o_rp, o_rk, o_rh, o_rn1, o_rn2};
-  }
   hipError_t e = hipMemcpy(d_probs, probs.data(), b_probs, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_d1, desc1, b_d1, hipMemcpyHostToDevice);
   if (e == hipSuccess && n2) e = hipMemcpy(d_d2, desc2, (size_t)n2 * dim * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = picp_launch_match_prep(nullptr, d_d1, n1, dim, q_h, q_n1, q_n2);
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
-  if (e == hipSuccess && order) {
-    // queries: perm and key only (the matcher reads their prep rows through perm)
-    e = picp_launch_match_order(nullptr, d_probs, n_problems, 0, d_d1, dim, q_h, q_n1, q_n2, o_qp, o_qk, nullptr,
-                                nullptr, nullptr);
-    if (e == hipSuccess)
-      e = picp_launch_match_order(nullptr, d_probs, n_problems, 1, d_d2, dim, r_h, r_n1, r_n2, o_rp, o_rk, o_rh,
-                                  o_rn1, o_rn2);
-  }
   if (e == hipSuccess)
     e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
-                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form, ks, d_part,
-                               order ? &ord : nullptr);
+                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form, ks, d_part);
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);

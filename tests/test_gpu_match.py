@@ -190,55 +190,3 @@ def test_match_reference_range_split(native, oracle, monkeypatch, ksplit):
     d1s[2], d2s[2] = d1[:700], d2
     for d1_, d2_, got in zip(d1s, d2s, native.match_points_batch(d1s, d2s)):
         _eq(got, oracle.match_points(d1_, d2_))
-
-
-@pytest.mark.parametrize("order", ["1", "0"])
-def test_match_key_window(native, oracle, monkeypatch, order):
-    """The accept-only form's key-ordered window (picp_launch_match_order; PICP_MATCH_ORDER=0 turns
-    it off): queries and references in the order of their first component, each block scanning
-    only the reference tiles within 1.001 sqrt(R) of its queries' keys.  Best matches displaced
-    along the key component alone to just inside dist_thr, hundreds of equal keys on both sides,
-    -0 / +0 keys, non-finite keys and components on both sides, the extreme keys (the first and
-    last blocks' windows), duplicates; ragged sets at the order kernel's size limit (8,192 rows
-    ordered, 8,193 not) and a forced reference-range split over the window."""
-    if _MODE["kernel"] != "accept_only":
-        pytest.skip("the window form is the accept-only form's")
-    monkeypatch.setenv("PICP_MATCH_ORDER", order)
-    rng = np.random.default_rng(99)
-    d2 = rng.uniform(-1, 1, (6000, 10)).astype(np.float32)
-    q = rng.uniform(-1, 1, (3000, 10)).astype(np.float32)
-    for k, delta in enumerate([0.4472, -0.4472, 0.447, 0.3, -0.3, 0.4471]):
-        d2[100 + k] = q[k]
-        d2[100 + k, 0] += np.float32(delta)          # d = delta^2: 0.19999... < dist_thr
-    q[10:30] = d2[200:220] + np.float32(0.01)
-    d2[300:700, 0] = 0.25                            # equal keys
-    q[30:400, 0] = 0.25
-    q[30:60] = d2[330:360]
-    d2[800, 0] = -0.0
-    d2[801, 0] = 0.0
-    q[400], q[401] = d2[800], d2[801]
-    d2[900, 0], d2[901, 0], d2[902, 0] = np.nan, np.inf, -np.inf
-    q[402, 0], q[403, 0] = np.nan, -np.inf
-    q[404] = d2[903]
-    q[404, 5] = np.nan
-    d2[1500, 0], d2[1501, 0] = -1.0, 1.0             # the extreme keys
-    q[405], q[406] = d2[1500], d2[1501]
-    d2[1000] = d2[1001]
-    q[407] = d2[1000]
-    q[408] = d2[2000]
-    q[408, 3] = 7e4                                  # a query beyond fp16 range
-    _eq(native.match_points(q, d2), oracle.match_points(q, d2))
-    monkeypatch.setenv("PICP_MATCH_KSPLIT", "3")
-    _eq(native.match_points(q[:700], d2), oracle.match_points(q[:700], d2))
-    monkeypatch.delenv("PICP_MATCH_KSPLIT")
-    for sizes in ([(2000, 8192), (5, 1), (0, 40), (8192, 300)], [(300, 8193), (20, 20)]):
-        d1s, d2s = [], []
-        for n1, n2 in sizes:
-            b = rng.uniform(-1, 1, (n2, 10)).astype(np.float32)
-            a = rng.uniform(-1, 1, (n1, 10)).astype(np.float32)
-            m = min(n1 // 2, n2)
-            a[:m] = b[rng.choice(n2, m, replace=False)] + rng.normal(0, 0.01, (m, 10)).astype(np.float32)
-            d1s.append(a)
-            d2s.append(b)
-        for a, b, got in zip(d1s, d2s, native.match_points_batch(d1s, d2s)):
-            _eq(got, oracle.match_points(a, b))
