@@ -156,12 +156,6 @@ typedef float mm_f16v __attribute__((ext_vector_type(16)));
 // The launcher takes RB = 2 when that still fills a generation of blocks (C5: +3.4 %,
 // 1024 x 2000 x 2000: -9 % time) and RB = 1 for small grids (64 x 2000 x 8000: RB = 2 +9 %).
 #define MM_CAP 16                 // candidate slots per query
-#ifndef MM_CAP4
-#define MM_CAP4 7                 // the same at RB = 4 (its lists in the LDS of four blocks per CU)
-#endif
-#ifndef MM_BT4
-#define MM_BT4 2                  // folded pass at RB = 4: column blocks per LDS wait
-#endif
 // Reference-range split (ksplit > 1): a problem's references in ranges of mm_kchunk rows, at least
 // MM_KMIN (so a range is worth a block's query prologue), whole tiles; mm_nsplit non-empty ranges.
 #define MM_KMIN 1024
@@ -342,7 +336,7 @@ __device__ __forceinline__ unsigned mm_pack16(unsigned m) {
 #define MM_MINB 1
 #endif
 template <int KCH, int RAD, int RB>
-__global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_mfma_kernel(
+__global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const float* __restrict__ q_desc, const float* __restrict__ r_desc,
     const _Float16* __restrict__ q_h, const float* __restrict__ q_n1,
     const _Float16* __restrict__ r_h, const float* __restrict__ r_n1, const float* __restrict__ r_n2,
@@ -352,9 +346,7 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
     int xcd_map, int ksplit, float4* __restrict__ part, int64_t part_nq) {
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
-  constexpr int BT = (RB == 4) ? MM_BT4 : (RB == 2) ? MM_BT2 : MM_BT;
-  constexpr int CAP = (RB == 4) ? MM_CAP4 : MM_CAP;  // candidate slots per query
-  constexpr int RBB = (RB == 4) ? 2 : 1;             // entry bits of the row block
+  constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
   constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
@@ -366,7 +358,7 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
     mm_half8 t[2][CH];                   // tile rows, 16-B chunks: row*(DP/8) + c*2 + h
     float n[2][2][MM_RT];                // [buf][n1|n2][ref]
     int cnt[MM_WAVES][QPW];
-    int list[MM_WAVES][QPW][CAP];
+    int list[MM_WAVES][QPW][MM_CAP];
     float nq[MM_WAVES][QPW];
   };
   __shared__ Lds lds;
@@ -423,12 +415,12 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
         if (16 * c + 8 * hf + e >= dim) qa[rb][c][e] = (_Float16)0.0f;
     }
   }
-  for (int ql = lane; ql < QPW; ql += 64) {  // (RB = 4: two queries per lane)
-    const int64_t qi = qw + ql;
+  if (lane < QPW) {
+    const int64_t qi = qw + lane;
     float nq = (qi < P.nq) ? q_n1[P.q_off + qi] : 0.0f;  // +inf: unsafe query
     if (RAD == 2 && !(nq <= MM_FOLD_MAX)) nq = INFINITY;  // outside the fold's range: full scan
-    s_nq[w][ql] = nq;
-    s_cnt[w][ql] = 0;
+    s_nq[w][lane] = nq;
+    s_cnt[w][lane] = 0;
   }
 
   const int64_t nr_all = P.nr;
@@ -609,7 +601,7 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
   // the reference.  After the pass the wave expands the entries into the per-query lists the
   // rescan reads (~1 candidate per query on C5, so a lane holds a few; a lane that overflows its
   // list sends every query of its wave to the full scan, as does a range past 4,096 tiles).
-  constexpr int LCAP = QPW * CAP / 64;  // RB = 2: 16, RB = 1: 8, RB = 4: 16
+  constexpr int LCAP = QPW * MM_CAP / 64;  // RB = 2: 16, RB = 1: 8
   static_assert(MM_RT / 32 <= 8, "column block index: 3 bits");
   int* const lane_list = &s_list[w][0][0] + lane * LCAP;
   int c_n = 0;
@@ -617,8 +609,7 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
   // so no kept entry is lost
   auto push_mask = [&](unsigned m16, int64_t t0, int cb, int rb) {
     if (m16) {
-      lane_list[min(c_n, LCAP - 1)] =
-          (int)((((unsigned)(t0 / MM_RT) << (3 + RBB) | (unsigned)cb << RBB | (unsigned)rb) << 16) | m16);
+      lane_list[min(c_n, LCAP - 1)] = (int)((((unsigned)(t0 / MM_RT) << 4 | (unsigned)cb << 1 | (unsigned)rb) << 16) | m16);
       ++c_n;
     }
   };
@@ -732,34 +723,32 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
     unsigned ent[LCAP];
 #pragma unroll
     for (int u = 0; u < LCAP; ++u) ent[u] = (u < ln) ? (unsigned)lane_list[u] : 0u;
-    const bool ovf = __any(c_n > LCAP) || nr_all > ((int64_t)MM_RT << (13 - RBB));
+    const bool ovf = __any(c_n > LCAP) || nr_all > ((int64_t)MM_RT << 12);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int u = 0; u < LCAP; ++u)
       if (u < ln) {
         const unsigned blk = ent[u] >> 16;
-        const int ref = (int)(blk >> (3 + RBB)) * MM_RT + (int)((blk >> RBB) & 7u) * 32 + r;
-        const int rbase = 32 * (int)(blk & ((1u << RBB) - 1u)) + 4 * hf;
+        const int ref = (int)(blk >> 4) * MM_RT + (int)((blk >> 1) & 7u) * 32 + r;
+        const int rbase = 32 * (int)(blk & 1u) + 4 * hf;
         unsigned m = ent[u] & 0xffffu;
         while (m) {
           const int i = __builtin_ctz(m);
           m &= m - 1;
           const int row = rbase + (i & 3) + 8 * (i >> 2);
           const int slot = atomicAdd(&s_cnt[w][row], 1);
-          if (slot < CAP) s_list[w][row][slot] = ref;
+          if (slot < MM_CAP) s_list[w][row][slot] = ref;
         }
       }
     // a dropped entry (full lane list) or a reference range past the packing: the full scan
-    if (ovf)
-      for (int ql = lane; ql < QPW; ql += 64) s_cnt[w][ql] = CAP + 1;
+    if (ovf && lane < QPW) s_cnt[w][lane] = MM_CAP + 1;
   }
   __syncthreads();
 
   // ---------------- exact update over the candidates, in index order ----------------
-  for (int ql = lane; ql < QPW; ql += 64) {
-  const int64_t qi = qw + ql;
-  if (qi < P.nq) {
+  const int64_t qi = qw + lane;
+  if (lane < QPW && qi < P.nq) {
     float q[DMAX];
 #pragma unroll
     for (int k = 0; k < DMAX; ++k) q[k] = (k < dim) ? q_desc[(P.q_off + qi) * dim + k] : 0.0f;
@@ -768,15 +757,15 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
 #ifdef MM_DIAG_NORESCAN  // diagnostic timing build only: no exact rescan
     const int n = 0;
 #else
-    const int n = s_cnt[w][ql];
+    const int n = s_cnt[w][lane];
 #endif
 #ifdef PICP_STAMPS
     atomicAdd(&picp_match_stats[2], 1ull);
     atomicAdd(&picp_match_stats[1], (unsigned long long)n);
     atomicMax(&picp_match_stats[3], (unsigned long long)n);
-    if (n > CAP || !(s_nq[w][ql] < INFINITY)) atomicAdd(&picp_match_stats[0], 1ull);
+    if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) atomicAdd(&picp_match_stats[0], 1ull);
 #endif
-    if (n > CAP || !(s_nq[w][ql] < INFINITY)) {  // slow path: the reference's full scan
+    if (n > MM_CAP || !(s_nq[w][lane] < INFINITY)) {  // slow path: the reference's full scan
       for (int64_t j = 0; j < P.nr; ++j) {
         const float d = mm_exact_dist(q, r_desc + (P.r_off + j) * dim, dim);
         if (d < best) { second = best; best = d; bi = (int32_t)j; }
@@ -798,7 +787,7 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
         int jj[MM_RQ];
 #pragma unroll
         for (int u = 0; u < MM_RQ; ++u) {
-          jj[u] = (k0 + u < n) ? s_list[w][ql][k0 + u] : -1;
+          jj[u] = (k0 + u < n) ? s_list[w][lane][k0 + u] : -1;
           const float* rp = r_desc + (P.r_off + max(jj[u], 0)) * dim;
 #pragma unroll
           for (int k = 0; k < DMAX; ++k) rr[u][k] = (jj[u] >= 0 && k < dim) ? rp[k] : 0.0f;
@@ -829,7 +818,6 @@ __global__ __launch_bounds__(MM_BLOCK, (RB == 4) ? 4 : MM_MINB) void picp_match_
     else
       match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
                   accepted);  // :100-103
-  }
   }
 }
 
@@ -915,7 +903,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   const int64_t blocks_rb2 = (int64_t)n_problems * ((max_nq + 2 * 32 * MM_WAVES - 1) / (2 * 32 * MM_WAVES));
   // (measured for the folded accept-only form only; the others need 130-224 VGPRs at RB = 2)
   int rb = (fold && blocks_rb2 >= 4 * (int64_t)num_cu) ? 2 : 1;
-  if (const char* e = getenv("PICP_MATCH_RB")) rb = (atoi(e) == 4 && fold) ? 4 : (atoi(e) == 2) ? 2 : 1;
+  if (const char* e = getenv("PICP_MATCH_RB")) rb = (atoi(e) == 2) ? 2 : 1;
   const int qpb = MM_WAVES * 32 * rb;
   const int gx = (int)((max_nq + qpb - 1) / qpb);
   const char* xe = getenv("PICP_MATCH_XCD");
@@ -934,8 +922,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
     else PICP_LAUNCH_MM3(KC, RD, 1);             \
   }
   if (dim <= 16) {
-    if (fold && rb == 4) PICP_LAUNCH_MM3(1, 2, 4);
-    else if (fold) PICP_LAUNCH_MM(1, 2)
+    if (fold) PICP_LAUNCH_MM(1, 2)
     else if (rad) PICP_LAUNCH_MM(1, 1)
     else PICP_LAUNCH_MM(1, 0)
   } else {
