@@ -80,16 +80,13 @@ extern "C" hipError_t picp_debug_bstamps(unsigned long long* out, size_t n_words
 // host's check).  Writes a.probs[s] (the append reads n) and returns n.
 struct NoVo {};
 #define VOG_CHUNKS 8  // observation chunks of BS held in registers: 4096 at BS 512
-// (the same 4096 observations at BS 1024: four chunks, within its 128-VGPR budget)
-__host__ __device__ constexpr int vog_chunks(int bs) { return bs >= 1024 ? 4 : VOG_CHUNKS; }
 #define VOG_SLICE 256  // items per pass of the register transfer
 template <int NPT, int BS>
 __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, float* xs, float* ys, float* zs,
                                                float* us, float* vs, float* lx, float* ly, float* lz,
                                                float* lu, float* lv, int lds_items) {
   constexpr int NW = BS / 64;
-  constexpr int VC = vog_chunks(BS);  // observation chunks of BS
-  __shared__ int s_wc[VC][NW];          // flagged observations per (chunk, wave)
+  __shared__ int s_wc[VOG_CHUNKS][NW];          // flagged observations per (chunk, wave)
   __shared__ float s_sl[5][VOG_SLICE];          // the items of one pass
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const VoSegment G = a.segs[s];
@@ -100,19 +97,19 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
     nn = a.frame_off[G.f0 + t + 2] - on;
   }
   // every chunk's loads first (accept flag, map index, pixel; then the map point)
-  bool fl[VC];
-  int jb[VC];
-  float px[VC], py[VC], pz[VC];
-  float2 pu[VC];
+  bool fl[VOG_CHUNKS];
+  int jb[VOG_CHUNKS];
+  float px[VOG_CHUNKS], py[VOG_CHUNKS], pz[VOG_CHUNKS];
+  float2 pu[VOG_CHUNKS];
 #pragma unroll
-  for (int c = 0; c < VC; ++c) {
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
     const int64_t i = (int64_t)c * BS + tid;
     fl[c] = i < nn && a.wm_acc[on + i] != 0;
     jb[c] = (i < nn) ? a.wm_bi[on + i] : 0;
     pu[c] = (i < nn) ? a.uv[on + i] : make_float2(0.0f, 0.0f);
   }
 #pragma unroll
-  for (int c = 0; c < VC; ++c) {
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
     const int64_t j = G.map_off + (fl[c] ? jb[c] : 0);
     px[c] = fl[c] ? a.map_xyz[3 * j + 0] : 0.0f;
     py[c] = fl[c] ? a.map_xyz[3 * j + 1] : 0.0f;
@@ -120,9 +117,9 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
   }
   // the ordered compaction of all chunks with one barrier: per (chunk, wave) counts, then each
   // flagged observation's output index = flagged before its chunk + before its wave + its lane rank
-  int rk[VC];
+  int rk[VOG_CHUNKS];
 #pragma unroll
-  for (int c = 0; c < VC; ++c) {
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
     const unsigned long long m = __ballot(fl[c]);
     rk[c] = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) s_wc[c][w] = __popcll(m);
@@ -130,7 +127,7 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
   __syncthreads();
   int n = 0;
 #pragma unroll
-  for (int c = 0; c < VC; ++c) {
+  for (int c = 0; c < VOG_CHUNKS; ++c) {
     int pre = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
@@ -143,7 +140,7 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
   // items past the registers go straight to the LDS stage
   const int r0 = NPT * BS;
 #pragma unroll
-  for (int c = 0; c < VC; ++c)
+  for (int c = 0; c < VOG_CHUNKS; ++c)
     if (fl[c] && rk[c] >= r0 && rk[c] - r0 < lds_items) {
       const int o = rk[c] - r0;
       lx[o] = px[c];
@@ -160,7 +157,7 @@ __device__ __forceinline__ int vo_gather_items(const VoArgs& a, int s, int t, fl
   float lastv[5];
   for (int q = 0; q <= qlast && q * VOG_SLICE < NPT * BS; ++q) {  // uniform: n is the block's
 #pragma unroll
-    for (int c = 0; c < VC; ++c)
+    for (int c = 0; c < VOG_CHUNKS; ++c)
       if (fl[c] && rk[c] / VOG_SLICE == q) {
         const int o = rk[c] - q * VOG_SLICE;
         s_sl[0][o] = px[c];
@@ -614,66 +611,41 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
 // step t, one 512-thread block each, npt register items per lane and the LDS stage sized for
 // max_obs (every item of a frame of <= max_obs observations is on-chip).  The caller checks
 // picp_vo_block_fusable(npt, max_obs) first; otherwise it runs vo_gather_kernel + the plain launch.
-// the LDS stage of a VO step block of bs threads: the frame's items past npt x bs, capped
-static size_t vo_lds_bytes(int npt, int bs, int max_obs, int* lds_items_out) {
-  const int lds_items = (max_obs > npt * bs) ? min(max_obs - npt * bs, PICP_BLDS_ITEMS) : 0;
-  if (lds_items_out) *lds_items_out = lds_items;
-  return (size_t)5 * lds_items * sizeof(float);
-}
-
-// bs: 512 threads (two waves per SIMD), or 1,024 (four per SIMD within 128 VGPRs; npt 1 or 2)
-extern "C" int picp_vo_block_fusable_bs(int npt, int bs, int64_t max_obs) {
-  int lds_items = 0;
-  vo_lds_bytes(npt, bs, (int)max_obs, &lds_items);
-  const bool shape = (bs == PICP_BBLOCK && (npt == 1 || npt == 2 || npt == 4 || npt == 8)) ||
-                     (bs == 2 * PICP_BBLOCK && (npt == 1 || npt == 2));
-  return shape && max_obs <= (int64_t)vog_chunks(bs) * bs && max_obs <= (int64_t)npt * bs + lds_items;
-}
 extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs) {
-  return picp_vo_block_fusable_bs(npt, PICP_BBLOCK, max_obs);
-}
-
-extern "C" hipError_t picp_launch_vo_block_bs(hipStream_t stream, const VoArgs* a, int t, int npt,
-                                              const PicpArgs* args, int64_t max_obs, int bs) {
-  if (!a || !args || a->n_seg <= 0 || !picp_vo_block_fusable_bs(npt, bs, max_obs)) return hipErrorInvalidValue;
   int lds_items = 0;
-  const size_t lds_bytes = vo_lds_bytes(npt, bs, (int)max_obs, &lds_items);
-  const int var = picp_variant(args->K, args->keep_outliers);
-#define PICP_LAUNCH_VB3(N, P, B, W)                                                                        \
-  {                                                                                                        \
-    if (lds_bytes > 65536)                                                                                 \
-      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, B, VoArgs, W>,                              \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);                     \
-    hipLaunchKernelGGL((picp_block_kernel<N, P, B, VoArgs, W>), dim3(a->n_seg), dim3(B), lds_bytes, stream, \
-                       a->X, a->Y, a->Z, a->U, a->V, *args, a->probs + a->seg0, a->st_in + a->seg0,          \
-                       (PicpState*)a->st_out + a->seg0, lds_items, 1, a->n_seg, nullptr, nullptr, nullptr,  \
-                       0ull, *a, t);                                                                       \
-  }
-#define PICP_LAUNCH_VB(N, B, W)                                                        \
-  if (var == PICP_V_PINHOLE) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE, B, W)                   \
-  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE_KEEP, B, W)    \
-  else PICP_LAUNCH_VB3(N, PICP_V_GENERAL, B, W)
-  if (bs == 2 * PICP_BBLOCK) {
-    switch (npt) {
-      case 1: PICP_LAUNCH_VB(1, 2 * PICP_BBLOCK, 4); break;
-      case 2: PICP_LAUNCH_VB(2, 2 * PICP_BBLOCK, 4); break;
-      default: return hipErrorInvalidValue;
-    }
-  } else {
-    switch (npt) {
-      case 1: PICP_LAUNCH_VB(1, PICP_BBLOCK, 2); break;
-      case 2: PICP_LAUNCH_VB(2, PICP_BBLOCK, 2); break;
-      case 4: PICP_LAUNCH_VB(4, PICP_BBLOCK, 2); break;
-      case 8: PICP_LAUNCH_VB(8, PICP_BBLOCK, 2); break;
-      default: return hipErrorInvalidValue;
-    }
-  }
-#undef PICP_LAUNCH_VB
-#undef PICP_LAUNCH_VB3
-  return hipGetLastError();
+  block_lds_bytes(npt, 1, (int)max_obs, &lds_items);
+  return max_obs <= (int64_t)VOG_CHUNKS * PICP_BBLOCK && max_obs <= (int64_t)npt * PICP_BBLOCK + lds_items &&
+         (npt == 1 || npt == 2 || npt == 4 || npt == 8);
 }
 
 extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
                                            const PicpArgs* args, int64_t max_obs) {
-  return picp_launch_vo_block_bs(stream, a, t, npt, args, max_obs, PICP_BBLOCK);
+  if (!a || !args || a->n_seg <= 0 || !picp_vo_block_fusable(npt, max_obs)) return hipErrorInvalidValue;
+  int lds_items = 0;
+  const size_t lds_bytes = block_lds_bytes(npt, 1, (int)max_obs, &lds_items);
+  const int var = picp_variant(args->K, args->keep_outliers);
+#define PICP_LAUNCH_VB3(N, P)                                                                              \
+  {                                                                                                        \
+    if (lds_bytes > 65536)                                                                                 \
+      hipFuncSetAttribute((const void*)picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>,                       \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);                     \
+    hipLaunchKernelGGL((picp_block_kernel<N, P, PICP_BBLOCK, VoArgs>), dim3(a->n_seg), dim3(PICP_BBLOCK),  \
+                       lds_bytes, stream, a->X, a->Y, a->Z, a->U, a->V, *args, a->probs + a->seg0,          \
+                       a->st_in + a->seg0, (PicpState*)a->st_out + a->seg0, lds_items, 1, a->n_seg,         \
+                       nullptr, nullptr, nullptr, 0ull, *a, t);                                            \
+  }
+#define PICP_LAUNCH_VB(N)                                                        \
+  if (var == PICP_V_PINHOLE) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE)                   \
+  else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_VB3(N, PICP_V_PINHOLE_KEEP)    \
+  else PICP_LAUNCH_VB3(N, PICP_V_GENERAL)
+  switch (npt) {
+    case 1: PICP_LAUNCH_VB(1); break;
+    case 2: PICP_LAUNCH_VB(2); break;
+    case 4: PICP_LAUNCH_VB(4); break;
+    case 8: PICP_LAUNCH_VB(8); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef PICP_LAUNCH_VB
+#undef PICP_LAUNCH_VB3
+  return hipGetLastError();
 }

@@ -30,9 +30,6 @@ extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int 
                                         unsigned int* tagbase, unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a, int t);
 extern "C" int picp_vo_block_fusable(int npt, int64_t max_obs);
-extern "C" int picp_vo_block_fusable_bs(int npt, int bs, int64_t max_obs);
-extern "C" hipError_t picp_launch_vo_block_bs(hipStream_t stream, const VoArgs* a, int t, int npt,
-                                              const PicpArgs* args, int64_t max_obs, int bs);
 extern "C" int picp_build_packed_fp32(void);
 extern "C" hipError_t picp_launch_vo_block(hipStream_t stream, const VoArgs* a, int t, int npt,
                                            const PicpArgs* args, int64_t max_obs);
@@ -73,7 +70,6 @@ struct picp_vo {
   float *obs_n1 = nullptr, *obs_n2 = nullptr;
   // segments
   int n_seg = 0, max_steps = 0, npt = 1;
-  int vo_bs = 512;  // the fused step block's threads (PICP_VO_BS=1024: four waves per SIMD, A/B)
   int64_t map_slots = 0, n_slots = 0, cap_c = 0;
   std::vector<VoSegment> segs;
   std::vector<MatchProblem> pprobs;
@@ -240,7 +236,6 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
-  if (const char* e = getenv("PICP_VO_BS")) h->vo_bs = (atoi(e) == 1024) ? 1024 : 512;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
@@ -395,7 +390,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   // 512 * npt slots the biggest frame fills (masked slots cost as much as live ones every
   // round; the few items past npt * 512 take the kernel's streamed-remainder path)
   int npt = 1;
-  while (npt < 8 && (int64_t)npt * 2 * h->vo_bs <= h->max_obs) npt *= 2;
+  while (npt < 8 && (int64_t)npt * 2 * 512 <= h->max_obs) npt *= 2;
 
   // one allocation for everything sized by the segments
   struct Part { size_t off, bytes; };
@@ -625,7 +620,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
 #ifdef PICP_VO_DIAG
   const bool fused = false;  // vo_snap and PICP_VO_DIAG_SKIP need the gather's planes and launch
 #else
-  const bool fused = h->fuse && picp_vo_block_fusable_bs(h->npt, h->vo_bs, h->max_obs);
+  const bool fused = h->fuse && picp_vo_block_fusable(h->npt, h->max_obs);
 #endif
   if (e == hipSuccess && C > 1) e = hipEventRecord(h->ev_cj[0], h->stream);  // fork
   // the chains' launches are enqueued step by step, chain after chain within a step: enqueued
@@ -656,7 +651,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
       if (e == hipSuccess && !(skip & 8)) e = world_match(st, V, h->wprobs_d, c);
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
       if (fused) {
-        if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block_bs(st, &V, t, h->npt, &h->pargs, h->max_obs, h->vo_bs);
+        if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs);
       } else {
         if (e == hipSuccess && !(skip & 1)) e = picp_launch_vo_gather(st, &V, t);
         if (e == hipSuccess && !(skip & 4))
