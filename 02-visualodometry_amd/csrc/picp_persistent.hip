@@ -41,6 +41,16 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #ifndef PICP_POSE_STAGGER
 #define PICP_POSE_STAGGER 8
 #endif
+// The solvers' sweep with two passes in flight, PICP_SWEEP_STAGGER x 64 clocks apart (0: one
+// pass at a time).  Each pass loads every pending granule pair (the others point past the buffer's
+// range: no memory access, a zero), so both passes' loads are unconditional and the waits count
+// exactly one pass.
+#ifndef PICP_SWEEP_STAGGER
+#define PICP_SWEEP_STAGGER 8
+#endif
+#ifndef PICP_SWEEP_MIN_NPT  // the staggered sweep from this many items per lane on
+#define PICP_SWEEP_MIN_NPT 2
+#endif
 #ifndef PICP_POSE_NPOLL  // polls in flight in the followers' pose wait (2 or 3), when staggered
 #define PICP_POSE_NPOLL 2
 #endif
@@ -263,6 +273,45 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         if (g + NG * i < nblk) pending |= 1u << i;
       }
       [[maybe_unused]] int npass = 0;  // sweep passes (diagnostic stamps)
+      constexpr int SWEEP_ST = (NPT >= PICP_SWEEP_MIN_NPT) ? PICP_SWEEP_STAGGER : 0;
+      if constexpr (SWEEP_ST > 0) {
+        u32x4 ga[MAXG], gb[MAXG];
+        auto issue = [&](u32x4* gg, unsigned want) {
+#pragma unroll
+          for (int i = 0; i < MAXG; ++i)
+            gg[i] = __builtin_amdgcn_raw_buffer_load_b128(
+                rsrc, (want & (1u << i)) ? ((g + NG * i) * PICP_NPART + 2 * c) * 8 : 0x7ffffff0, 0,
+                PICP_AUX_SC1_VOLATILE);
+        };
+        auto take = [&](const u32x4* gg, unsigned want) {
+#pragma unroll
+          for (int i = 0; i < MAXG; ++i)
+            if ((want & pending & (1u << i)) && gg[i][1] == tbase + epoch && gg[i][3] == tbase + epoch) {
+              gv[i] = gg[i];
+              pending &= ~(1u << i);
+            }
+        };
+        unsigned wa = pending, wb;
+        issue(ga, wa);
+        __builtin_amdgcn_s_sleep(SWEEP_ST);
+        wb = pending;
+        issue(gb, wb);
+        for (;;) {
+          take(ga, wa);
+          if (!pending) break;
+          wa = pending;
+          issue(ga, wa);
+          take(gb, wb);
+          if (!pending) break;
+          wb = pending;
+          issue(gb, wb);
+          if (timed_out(deadline)) {
+            __hip_atomic_store(errw, 1u, RLX_AGENT);
+            s_tmo = 1;
+            break;
+          }
+        }
+      } else {
       for (;;) {
         const unsigned want = pending;  // issue every pending load before checking any tag
         SWSTAMP(2 * npass);
@@ -283,6 +332,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           break;
         }
         PICP_POLL_PAUSE();
+      }
       }
       double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
