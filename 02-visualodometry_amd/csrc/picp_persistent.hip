@@ -44,7 +44,8 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 // The solvers' sweep with two passes in flight, PICP_SWEEP_STAGGER x 64 clocks apart (0: one
 // pass at a time).  Each pass loads every pending granule pair (the others point past the buffer's
 // range: no memory access, a zero), so both passes' loads are unconditional and the waits count
-// exactly one pass.
+// exactly one pass.  C3 150.5k -> 156.5k it/s (8 x 64 clocks; 16: 155k); with one item per lane
+// (C2) -2 %, so it starts at PICP_SWEEP_MIN_NPT items (profiles/r05/sweep_stagger/).
 #ifndef PICP_SWEEP_STAGGER
 #define PICP_SWEEP_STAGGER 8
 #endif
