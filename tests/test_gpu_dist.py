@@ -100,9 +100,10 @@ def test_refused_residency_selects_layout_without_handoffs(native, oracle, sizes
         assert synth.se3_log_norm(P[i], b2.poses()[i]) < POSE_TOL, i
 
 
-@pytest.mark.parametrize("sizes", [[100000], [10000] * 128])
+@pytest.mark.parametrize("sizes", [[100000], [300000], [10000] * 128])
 def test_timed_out_handoff_reruns_without_handoffs(native, oracle, sizes):
     """Every hand-off wait expires (PICP_TIMEOUT_MS = 1e-4 ms): the persistent / split-block launch
+    (300k: four items per lane, the solvers' staggered sweep)
     ends with the error word set, the library lays the batch out without hand-offs, re-runs the
     same solve from the same initial poses and returns the oracle's pose; fallbacks counts it and
     later solves keep the safe layout."""
