@@ -313,27 +313,27 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           }
         }
       } else {
-      for (;;) {
-        const unsigned want = pending;  // issue every pending load before checking any tag
-        SWSTAMP(2 * npass);
+        for (;;) {
+          const unsigned want = pending;  // issue every pending load before checking any tag
+          SWSTAMP(2 * npass);
 #pragma unroll
-        for (int i = 0; i < MAXG; ++i)
-          if (want & (1u << i))
-            gv[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((g + NG * i) * PICP_NPART + 2 * c) * 8, 0,
-                                                           PICP_AUX_SC1_VOLATILE);
+          for (int i = 0; i < MAXG; ++i)
+            if (want & (1u << i))
+              gv[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((g + NG * i) * PICP_NPART + 2 * c) * 8, 0,
+                                                             PICP_AUX_SC1_VOLATILE);
 #pragma unroll
-        for (int i = 0; i < MAXG; ++i)
-          if ((want & (1u << i)) && gv[i][1] == tbase + epoch && gv[i][3] == tbase + epoch) pending &= ~(1u << i);
-        SWSTAMP(2 * npass + 1);
-        ++npass;
-        if (!pending) break;
-        if (timed_out(deadline)) {
-          __hip_atomic_store(errw, 1u, RLX_AGENT);
-          s_tmo = 1;
-          break;
+          for (int i = 0; i < MAXG; ++i)
+            if ((want & (1u << i)) && gv[i][1] == tbase + epoch && gv[i][3] == tbase + epoch) pending &= ~(1u << i);
+          SWSTAMP(2 * npass + 1);
+          ++npass;
+          if (!pending) break;
+          if (timed_out(deadline)) {
+            __hip_atomic_store(errw, 1u, RLX_AGENT);
+            s_tmo = 1;
+            break;
+          }
+          PICP_POLL_PAUSE();
         }
-        PICP_POLL_PAUSE();
-      }
       }
       double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
