@@ -14,8 +14,13 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const struct MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted, int form, int ksplit,
-                                             float4* part);
+                                             float4* part, int64_t part_cap);
+// picp_match_ksplit reads PICP_MATCH_KSPLIT each call; picp_match_ksplit_forced takes the forced
+// count (0: none) from the caller, so a handle can read the variable once and size its scratch and
+// its launches from the same value
 extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form);
+extern "C" int picp_match_ksplit_forced(int n_problems, int64_t max_nq, int64_t max_nr, int form, int force);
+extern "C" int picp_match_ksplit_env(void);
 extern "C" int picp_match_prep_kch(int dim);
 
 // records the thread's last error message (picp_last_error) and returns `code`

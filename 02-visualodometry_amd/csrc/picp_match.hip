@@ -159,7 +159,8 @@ typedef float mm_f16v __attribute__((ext_vector_type(16)));
 // Reference-range split (ksplit > 1): a problem's references in ranges of mm_kchunk rows, at least
 // MM_KMIN (so a range is worth a block's query prologue), whole tiles; mm_nsplit non-empty ranges.
 #define MM_KMIN 1024
-#define MM_KSPLIT_MAX 16
+#define MM_KSPLIT_MAX 16        // the occupancy split's cap (picp_match_ksplit)
+#define MM_KSPLIT_LIMIT 65536   // a launch's hard limit (reference sets up to 2^36 rows in 2^20-row ranges)
 __host__ __device__ __forceinline__ int64_t mm_kchunk(int64_t nr, int ksplit) {
   const int64_t c = (nr + ksplit - 1) / ksplit;
   const int64_t t = (c + 255) / 256 * 256;
@@ -877,9 +878,11 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              const MatchProblem* probs, int dim, float dist_thr,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted, int form, int ksplit,
-                                             float4* part) {
+                                             float4* part, int64_t part_cap) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
-  if (ksplit < 1 || ksplit > MM_KSPLIT_MAX || (ksplit > 1 && !part)) return hipErrorInvalidValue;
+  // part_cap: the scratch's capacity in float4; a split launch writes ksplit x n_problems x max_nq
+  if (ksplit < 1 || ksplit > MM_KSPLIT_LIMIT) return hipErrorInvalidValue;
+  if (ksplit > 1 && (!part || (int64_t)ksplit * n_problems * max_nq > part_cap)) return hipErrorInvalidValue;
   const bool accept_only = (form & 1) != 0;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
   // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
@@ -909,6 +912,8 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   const char* xe = getenv("PICP_MATCH_XCD");
   const int xcd_map = (xe && atoi(xe) == 0) ? 0 : 1;
   const int64_t ngroups = (int64_t)n_problems * ksplit;
+  // the kernel decodes blockIdx.x in 32-bit unsigned arithmetic
+  if (8 * ((ngroups + 7) / 8) * gx > INT32_MAX || (int64_t)gx * ksplit > INT32_MAX) return hipErrorInvalidValue;
   const dim3 g = xcd_map ? dim3((unsigned)(8 * ((ngroups + 7) / 8) * gx))
                          : dim3((unsigned)(gx * ksplit), (unsigned)n_problems);
   const int64_t part_nq = max_nq;
@@ -942,12 +947,15 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
 }
 
 // The reference-range split a launch of this shape takes (1: none): enough (problem, query block,
-// range) blocks for about four per CU, at most MM_KSPLIT_MAX ranges.  The caller provides
-// ksplit x n_problems x max_nq float4 of scratch (picp_launch_match_mfma's part) when > 1.
-// PICP_MATCH_KSPLIT=n forces n (1: no split; A/B).  Small problem counts against large reference
-// sets (the VO world match of a few long segments: 8 x 2,000 queries x ~1.9e5 map points) would
-// otherwise run one block per CU or fewer.
-extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form) {
+// range) blocks for about four per CU, at most MM_KSPLIT_MAX ranges for occupancy -- and always
+// enough ranges that none exceeds the candidate entries' 2^20 references (4,096 tiles), however
+// many that takes (up to MM_KSPLIT_LIMIT): a range past the packing would send every query to the
+// O(nr) full scan.  The caller provides ksplit x n_problems x max_nq float4 of scratch
+// (picp_launch_match_mfma's part / part_cap) when > 1.  force > 0 replaces the occupancy choice
+// (PICP_MATCH_KSPLIT=n, read by picp_match_ksplit_env; 1: no occupancy split, A/B).  Small problem
+// counts against large reference sets (the VO world match of a few long segments: 8 x 2,000
+// queries x ~1.9e5 map points) would otherwise run one block per CU or fewer.
+extern "C" int picp_match_ksplit_forced(int n_problems, int64_t max_nq, int64_t max_nr, int form, int force) {
   if (form & 2) return 1;  // the exact scan is not split
   static int num_cu = 0;
   if (!num_cu) {
@@ -958,11 +966,20 @@ extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr,
   }
   const int64_t base = (int64_t)n_problems * ((max_nq + 32 * MM_WAVES - 1) / (32 * MM_WAVES));
   int64_t k = (4 * (int64_t)num_cu + base - 1) / std::max<int64_t>(base, 1);
-  if (const char* e = getenv("PICP_MATCH_KSPLIT")) k = atoi(e);
-  // a range's candidate entries index at most 4,096 tiles (2^20 references; larger ranges take the
-  // full scan): split the largest set at least that far
-  k = std::max<int64_t>(k, (max_nr + ((int64_t)MM_RT << 12) - 1) / ((int64_t)MM_RT << 12));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(k, MM_KSPLIT_MAX));
+  if (force > 0) k = force;
+  k = std::max<int64_t>(1, std::min<int64_t>(k, MM_KSPLIT_MAX));
+  // the entries' range: split the largest set at least that far (beyond the occupancy cap)
+  const int64_t k_range = (max_nr + ((int64_t)MM_RT << 12) - 1) / ((int64_t)MM_RT << 12);
+  return (int)std::min<int64_t>(std::max<int64_t>(k, k_range), MM_KSPLIT_LIMIT);
+}
+
+extern "C" int picp_match_ksplit_env(void) {
+  const char* e = getenv("PICP_MATCH_KSPLIT");
+  return e ? std::max(0, atoi(e)) : 0;
+}
+
+extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form) {
+  return picp_match_ksplit_forced(n_problems, max_nq, max_nr, form, picp_match_ksplit_env());
 }
 
 extern "C" hipError_t picp_launch_match(hipStream_t stream, int n_problems, int64_t max_nq,

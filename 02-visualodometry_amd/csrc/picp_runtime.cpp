@@ -1539,7 +1539,8 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)
     e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
-                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form, ks, d_part);
+                               dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form, ks, d_part,
+                               ks > 1 ? (int64_t)ks * n_problems * max_nq : 0);
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <utility>
 #include <vector>
 
 #include "picp_c.h"
@@ -108,9 +109,14 @@ struct picp_vo {
   // the matcher's reference-range split (picp_match_ksplit) for launches of few problems: each
   // chain's world match has its own scratch (the chains run concurrently), the frame->next
   // launches one between them (they run in stream order: chunk 0, then the side stream's)
+  // Every launch's split count is fixed at picp_vo_set_segments (PICP_MATCH_KSPLIT read once there)
+  // and the scratch sized from the same counts: a launch never uses more ranges than its scratch holds.
   std::vector<int> ks_w;          // [chains]
   std::vector<float4*> part_w;    // [chains]
+  std::vector<int64_t> cap_w;     // [chains]: part_w's capacity, float4
+  std::vector<std::pair<size_t, int>> ks_p;  // frame->next launch starting at problem .first: split .second
   float4* part_p = nullptr;
+  int64_t cap_p = 0;
   // the step's gather runs inside the PICP block kernel (picp_launch_vo_block) when every frame's
   // items fit on-chip; PICP_VO_FUSE=0 keeps vo_gather_kernel + the plain block launch (A/B: the
   // same items in the same order, the same bits)
@@ -414,25 +420,37 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_mn1 = part((size_t)map_slots * sizeof(float));
   const Part p_mn2 = part((size_t)map_slots * sizeof(float));
   // split scratch: each chain's world match (its n_seg_c problems) and the frame->next launches
+  const int ks_force = picp_match_ksplit_env();
   std::vector<int> ks_w((size_t)chains_eff, 1);
+  std::vector<int64_t> cap_w((size_t)chains_eff, 0);
   std::vector<Part> p_partw;
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
-    ks_w[c] = picp_match_ksplit(nsc, h->max_obs, max_map, h->accept_only);
-    p_partw.push_back(part(ks_w[c] > 1 ? (size_t)ks_w[c] * nsc * h->max_obs * sizeof(float4) : 0));
+    ks_w[c] = picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only, ks_force);
+    cap_w[c] = ks_w[c] > 1 ? (int64_t)ks_w[c] * nsc * h->max_obs : 0;
+    p_partw.push_back(part((size_t)cap_w[c] * sizeof(float4)));
   }
-  size_t part_p_bytes = 0;
+  // the frame->next launches, as vo_frame_match issues them: the whole table up front (overlap off)
+  // or chunk by chunk, each in launches of at most VO_MAX_GRID_Y problems
+  std::vector<std::pair<size_t, int>> ks_p;
+  int64_t cap_p = 0;
   {
-    auto need = [&](size_t np) {
-      for (size_t q = 0; q < np; q += VO_MAX_GRID_Y) {
-        const int n = (int)std::min<size_t>(VO_MAX_GRID_Y, np - q);
-        const int k = picp_match_ksplit(n, h->max_obs, h->max_obs, h->accept_only);
-        if (k > 1) part_p_bytes = std::max(part_p_bytes, (size_t)k * n * h->max_obs * sizeof(float4));
+    auto plan = [&](size_t p0, size_t p1) {
+      for (size_t q = p0; q < p1; q += VO_MAX_GRID_Y) {
+        const int n = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - q);
+        const int k = picp_match_ksplit_forced(n, h->max_obs, h->max_obs, h->accept_only, ks_force);
+        ks_p.emplace_back(q, k);
+        if (k > 1) cap_p = std::max(cap_p, (int64_t)k * n * h->max_obs);
       }
     };
-    need(pprobs.size());  // the frame->next matches up front (overlap off)
-    for (size_t k = 0; k + 1 < chunk_off.size(); ++k) need(chunk_off[k + 1] - chunk_off[k]);
+    const size_t nck = chunk_off.size() - 1;
+    if (h->overlap && nck > 1) {
+      for (size_t k = 0; k < nck; ++k) plan(chunk_off[k], chunk_off[k + 1]);
+    } else {
+      plan(0, pprobs.size());
+    }
   }
+  const size_t part_p_bytes = (size_t)cap_p * sizeof(float4);
   const Part p_partp = part(part_p_bytes);
   HIP_TRY(vo_malloc(h, &h->seg_mem, total, "segments"));
   HIP_TRY(hipMemset(h->seg_mem, 0, total));  // every table defined before the first run
@@ -442,6 +460,9 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   h->chunk_off = chunk_off;
   h->chains_eff = chains_eff;
   h->ks_w = ks_w;
+  h->cap_w = cap_w;
+  h->ks_p = ks_p;
+  h->cap_p = cap_p;
   h->part_w.assign((size_t)chains_eff, nullptr);
   for (int c = 0; c < chains_eff; ++c)
     if (p_partw[c].bytes) h->part_w[c] = (float4*)(m + p_partw[c].off);
@@ -525,10 +546,12 @@ static hipError_t vo_frame_match(picp_vo* h, hipStream_t st, size_t p0, size_t p
   hipError_t e = hipSuccess;
   for (; p0 < p1 && e == hipSuccess; p0 += VO_MAX_GRID_Y) {
     const int np = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - p0);
-    const int ks = h->part_p ? picp_match_ksplit(np, h->max_obs, h->max_obs, h->accept_only) : 1;
+    // the split planned for this launch at set_segments (a launch it did not plan runs unsplit)
+    auto it = std::lower_bound(h->ks_p.begin(), h->ks_p.end(), std::make_pair(p0, 0));
+    const int ks = (it != h->ks_p.end() && it->first == p0) ? it->second : 1;
     e = picp_launch_match_mfma(st, np, h->max_obs, h->desc_d, h->desc_d, h->obs_h, h->obs_n1, h->obs_h,
                                h->obs_n1, h->obs_n2, h->pprobs_d + p0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
-                               h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only, ks, h->part_p);
+                               h->pm_bi, h->pm_bd, h->pm_sd, h->pm_acc, h->accept_only, ks, h->part_p, h->cap_p);
   }
   return e;
 }
@@ -615,7 +638,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
     return picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
                                   V.map_n1, V.map_n2, probs + V.seg0, h->dim, VO_MATCH_DIST, VO_MATCH_RATIO,
                                   h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc, h->accept_only,
-                                  h->part_w[c] ? h->ks_w[c] : 1, h->part_w[c]);
+                                  h->part_w[c] ? h->ks_w[c] : 1, h->part_w[c], h->cap_w[c]);
   };
 #ifdef PICP_VO_DIAG
   const bool fused = false;  // vo_snap and PICP_VO_DIAG_SKIP need the gather's planes and launch
