@@ -190,3 +190,30 @@ def test_match_reference_range_split(native, oracle, monkeypatch, ksplit):
     d1s[2], d2s[2] = d1[:700], d2
     for d1_, d2_, got in zip(d1s, d2s, native.match_points_batch(d1s, d2s)):
         _eq(got, oracle.match_points(d1_, d2_))
+
+
+def test_match_past_2_24_references(native, oracle):
+    """A reference set past 2^24 rows: the candidate entries index 2^20 references per
+    range, so picp_match_ksplit splits such a set into more than MM_KSPLIT_MAX (16) ranges rather
+    than send every query to the O(nr) full scan.  64 queries x (2^24 + 4,099) references: exact
+    copies of references in the first, a middle and the last range (one duplicated across two
+    ranges: 0/0 ratio -> reject, the lower index first), near-copies and far queries; every output
+    bit-exact in all three forms."""
+    rng = np.random.default_rng(2024)
+    n_r, dim = (1 << 24) + 4099, 10
+    r = rng.uniform(-1, 1, (n_r, dim)).astype(np.float32)
+    src = np.array([3, 1 << 20, (1 << 20) + 1, 5_000_000, 9_999_999, 1 << 24, n_r - 1, 12_345_678])
+    r[(1 << 24) + 7] = r[9_999_999]  # a duplicate in another range
+    q = np.concatenate([r[src], r[src] + rng.uniform(-3e-3, 3e-3, (len(src), dim)).astype(np.float32),
+                        rng.uniform(-1, 1, (64 - 2 * len(src), dim)).astype(np.float32)])
+    ref = oracle.match_points(q, r)
+    assert ref["accepted"].sum() >= len(src) - 1 and not ref["accepted"][4]
+    for form in ("full", "exact", "accept_only"):
+        got = native.match_points_batch([q], [r], form=form)[0]
+        acc = ref["accepted"]
+        np.testing.assert_array_equal(got["accepted"].astype(bool), acc)
+        np.testing.assert_array_equal(got["best_idx"][acc], ref["best_idx"][acc])
+        if form != "accept_only":
+            np.testing.assert_array_equal(got["best_idx"], ref["best_idx"])
+            np.testing.assert_array_equal(got["best_dist"].view(np.uint32), ref["best_dist"].view(np.uint32))
+            np.testing.assert_array_equal(got["second_dist"].view(np.uint32), ref["second_dist"].view(np.uint32))
