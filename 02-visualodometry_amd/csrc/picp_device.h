@@ -1252,21 +1252,26 @@ __device__ __forceinline__ void finish_round(const PicpArgs& A, const PicpState&
 }
 
 
-// Two-view linear (DLT) triangulation of one point, cv::triangulatePoints as called from
-// src/cam.cpp:115 then convertPointsFromHomogeneous :118.  P1, P2: 3x4 ROW-major float.
-// A (4x4) in double, right singular vector of the smallest singular value by one-sided
+// Refined hardware reciprocal and reciprocal square root in double: the v_rcp_f64 / v_rsq_f64
+// estimate and two Newton steps (full double precision), half the dependency chain of the IEEE
+// division / sqrt sequences.
+__device__ __forceinline__ double tri_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double tri_rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
+  return fma(0.5 * y, fma(-x * y, y, 1.0), y);
+}
+
+// Right singular vector of the smallest singular value of the 4x4 DLT system A, by one-sided
 // (Hestenes) Jacobi, at most 10 sweeps, stopping after the first sweep that rotates nothing
 // (every later sweep would be a no-op); all indices compile-time so A and V stay in registers.
-__device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 a, float2 b,
-                                       float out[3]) {
-  double A[4][4], Vm[4][4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    A[0][k] = (double)a.x * (double)P1[8 + k] - (double)P1[0 + k];
-    A[1][k] = (double)a.y * (double)P1[8 + k] - (double)P1[4 + k];
-    A[2][k] = (double)b.x * (double)P2[8 + k] - (double)P2[0 + k];
-    A[3][k] = (double)b.y * (double)P2[8 + k] - (double)P2[4 + k];
-  }
+// A is consumed.
+__device__ __forceinline__ void tri_null_jacobi(double A[4][4], double v[4]) {
+  double Vm[4][4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1285,29 +1290,13 @@ __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 
         gamma += A[k][p] * A[k][qq];
       }
       // Rotate unless the pair is orthogonal to 1e-12 relative (gamma^2 <= 1e-24 alpha beta): the
-      // smaller rotations move the result below float precision, and the last sweeps of a
-      // 1e-17 threshold were a third of the append kernel's time.  Reciprocals and square roots
-      // are the hardware estimates refined by two Newton steps each (full double precision)
-      // instead of IEEE division and sqrt sequences: the rotation's dependency chain is half
-      // as long.  C5 759k -> 803k frames/s, the append 43.6 -> 24.8 us per launch
-      // (profiles/r05/tri_fast/); parity with the oracle's IEEE Jacobi at 1e-17
-      // is the tests' 1e-5 / 1e-4 relative (test_triangulation_matches_oracle_and_world).
+      // smaller rotations move the result below float precision.
       if (fabs(gamma) > 1e-300 && gamma * gamma > 1e-24 * (alpha * beta)) {
         rotated = true;
-        auto rcp = [](double x) {
-          double r = __builtin_amdgcn_rcp(x);
-          r = fma(r, fma(-x, r, 1.0), r);
-          return fma(r, fma(-x, r, 1.0), r);
-        };
-        auto rsq = [](double x) {
-          double y = __builtin_amdgcn_rsq(x);
-          y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
-          return fma(0.5 * y, fma(-x * y, y, 1.0), y);
-        };
-        const double zeta = (beta - alpha) * rcp(2.0 * gamma);
+        const double zeta = (beta - alpha) * tri_rcp(2.0 * gamma);
         const double q = fma(zeta, zeta, 1.0);
-        const double t = ((zeta >= 0.0) ? 1.0 : -1.0) * rcp(fabs(zeta) + q * rsq(q));  // 1/(|z| + sqrt(1+z^2))
-        const double c = rsq(fma(t, t, 1.0));
+        const double t = ((zeta >= 0.0) ? 1.0 : -1.0) * tri_rcp(fabs(zeta) + q * tri_rsq(q));  // 1/(|z| + sqrt(1+z^2))
+        const double c = tri_rsq(fma(t, t, 1.0));
         const double s = c * t;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1326,18 +1315,82 @@ __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 
 #pragma unroll
   for (int c = 0; c < 4; ++c) nrm[c] = A[0][c] * A[0][c] + A[1][c] * A[1][c] + A[2][c] * A[2][c] + A[3][c] * A[3][c];
   double best = nrm[0];
-  double v0 = Vm[0][0], v1 = Vm[1][0], v2 = Vm[2][0], v3 = Vm[3][0];
+  v[0] = Vm[0][0]; v[1] = Vm[1][0]; v[2] = Vm[2][0]; v[3] = Vm[3][0];
 #pragma unroll
   for (int c = 1; c < 4; ++c) {
     const bool take = nrm[c] < best;
     best = take ? nrm[c] : best;
-    v0 = take ? Vm[0][c] : v0;
-    v1 = take ? Vm[1][c] : v1;
-    v2 = take ? Vm[2][c] : v2;
-    v3 = take ? Vm[3][c] : v3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = take ? Vm[r][c] : v[r];
   }
+}
+
+// Two-view linear (DLT) triangulation of one point, cv::triangulatePoints as called from
+// src/cam.cpp:115 then convertPointsFromHomogeneous :118.  P1, P2: 3x4 ROW-major float.
+// A (4x4) in double; X_h = the right singular vector of A's smallest singular value, by the
+// one-sided Jacobi above (tri_null_jacobi).
+// -DPICP_TRI_INVIT (A/B, measured slower, not the default): the eigenvector of the smallest
+// eigenvalue of M = A^T A by inverse iteration on M through its
+// LDL^T (no pivoting: M is positive semi-definite and, for a finite point, its null direction has
+// w != 0, so the near-zero pivot is the last): x1 = M^-1 e4 (back substitution alone), then
+// x2 = M^-1 x1.  x2 is accepted when it moved less than ~1.4e-6 rad from x1 (1 - |cos| < 1e-12):
+// the error left after the second step is then below ~1e-12, the SVD's own rounding level.  A
+// point whose system is not that well separated (near-parallel rays, a point at infinity, a
+// degenerate ray pair, |w| <= 1e-5) takes the Jacobi SVD.  On the VO sequence's pairs (sigma4 / sigma3 ~1e-7)
+// every point takes the fast path, within 2.1e-11 of numpy's SVD.  Parity green (the long-segment
+// rule included), but the append got slower, not faster: C5 805k -> 777k frames/s, the N = 8
+// per-rank shape 161.4k -> 159.2k, 8e 42.7k -> 42.0k (profiles/r06/t1/ab_tri.log).
+__device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 a, float2 b,
+                                       float out[3]) {
+  double A[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    A[0][k] = (double)a.x * (double)P1[8 + k] - (double)P1[0 + k];
+    A[1][k] = (double)a.y * (double)P1[8 + k] - (double)P1[4 + k];
+    A[2][k] = (double)b.x * (double)P2[8 + k] - (double)P2[0 + k];
+    A[3][k] = (double)b.y * (double)P2[8 + k] - (double)P2[4 + k];
+  }
+  double v[4];
+#ifndef PICP_TRI_INVIT
+  tri_null_jacobi(A, v);
+#else
+  {
+    double M[4][4];  // upper triangle used
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = i; j < 4; ++j) M[i][j] = A[0][i] * A[0][j] + A[1][i] * A[1][j] + A[2][i] * A[2][j] + A[3][i] * A[3][j];
+    const double r0 = tri_rcp(M[0][0]);
+    const double l10 = M[0][1] * r0, l20 = M[0][2] * r0, l30 = M[0][3] * r0;
+    const double d1 = M[1][1] - l10 * M[0][1];
+    const double r1 = tri_rcp(d1);
+    const double l21 = (M[1][2] - l20 * M[0][1]) * r1, l31 = (M[1][3] - l30 * M[0][1]) * r1;
+    const double d2 = M[2][2] - l20 * M[0][2] - l21 * l21 * d1;
+    const double r2 = tri_rcp(d2);
+    const double l32 = (M[2][3] - l30 * M[0][2] - l31 * l21 * d1) * r2;
+    double d3 = M[3][3] - l30 * M[0][3] - l31 * l31 * d1 - l32 * l32 * d2;
+    d3 = (fabs(d3) > 1e-300) ? d3 : 1e-300;  // an exactly singular M: any tiny pivot gives its null vector
+    const double r3 = tri_rcp(d3);
+    // x1 = M^-1 e4 = L^-T (e4 / d3), normalised
+    double x3 = r3, x2 = -l32 * x3, x1 = -l21 * x2 - l31 * x3, x0 = -l10 * x1 - l20 * x2 - l30 * x3;
+    double s = tri_rsq(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
+    x0 *= s; x1 *= s; x2 *= s; x3 *= s;
+    // x2' = M^-1 x1: forward L y = x1, then L^T x = y / d
+    const double y0 = x0, y1 = x1 - l10 * y0, y2 = x2 - l20 * y0 - l21 * y1,
+                 y3 = x3 - l30 * y0 - l31 * y1 - l32 * y2;
+    const double z3 = y3 * r3, z2 = y2 * r2 - l32 * z3, z1 = y1 * r1 - l21 * z2 - l31 * z3,
+                 z0 = y0 * r0 - l10 * z1 - l20 * z2 - l30 * z3;
+    s = tri_rsq(z0 * z0 + z1 * z1 + z2 * z2 + z3 * z3);
+    v[0] = z0 * s; v[1] = z1 * s; v[2] = z2 * s; v[3] = z3 * s;
+    const double c = fabs(v[0] * x0 + v[1] * x1 + v[2] * x2 + v[3] * x3);
+    // (|w| well above FLT_EPSILON: the dehomogenisation below is then sign-independent)
+    const bool ok = (c > 1.0 - 1e-12) && (c <= 1.0 + 1e-12) && (d1 > 0.0) && (d2 > 0.0) && (M[0][0] > 0.0) &&
+                    (fabs(v[3]) > 1e-5);
+    if (!ok) tri_null_jacobi(A, v);  // rare: the fallback runs with the lanes that need it
+  }
+#endif
   // points4D is float; convertPointsFromHomogeneous in float, scale 1 when |w| <= FLT_EPSILON
-  const float X4 = (float)v0, Y4 = (float)v1, Z4 = (float)v2, W4 = (float)v3;
+  const float X4 = (float)v[0], Y4 = (float)v[1], Z4 = (float)v[2], W4 = (float)v[3];
   const float scale = (fabsf(W4) > FLT_EPSILON) ? 1.0f / W4 : 1.0f;
   out[0] = X4 * scale;
   out[1] = Y4 * scale;

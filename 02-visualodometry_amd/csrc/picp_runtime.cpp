@@ -981,6 +981,13 @@ extern "C" int picp_batch_residency(picp_batch_t* b, int* grid, int* resident, i
   return PICP_OK;
 }
 
+static void gather_to_poses(const PicpState* all, int64_t n_total, float* T_all, picp_stats* st_all) {
+  for (int64_t k = 0; k < n_total; ++k) {
+    state_to_pose(all[k], T_all + 16 * k);
+    if (st_all) state_to_stats(all[k], st_all[k]);
+  }
+}
+
 // Gather every rank's results of the batch split: this rank's batch holds the
 // problems picp_shard_range(n_total, world, rank) gives it; after its solve, one RCCL all-gather
 // of the 128-B per-problem states (on the batch's stream, device to device over xGMI) and one
@@ -1022,10 +1029,48 @@ extern "C" int picp_batch_allgather(picp_batch_t* b, picp_comm_t* c, int64_t n_t
   HIP_TRY(hipStreamSynchronize(b->stream));
   rc = picp_shard_unpack(n_total, world, sizeof(PicpState), padded.data(), all.data());
   if (rc) return rc;
-  for (int64_t k = 0; k < n_total; ++k) {
-    state_to_pose(all[(size_t)k], T_all + 16 * k);
-    if (st_all) state_to_stats(all[(size_t)k], st_all[k]);
+  gather_to_poses(all.data(), n_total, T_all, st_all);
+  return PICP_OK;
+}
+
+// The gather with a caller-supplied byte exchange (include/picp_c.h): the same shard check,
+// completion and padded state layout as picp_batch_allgather, staged through host memory.  Each
+// rank's send buffer is [16-B header: int32 status][maxn states]; one exchange carries both, so
+// the failure agreement needs no second collective.
+extern "C" int picp_batch_allgather_host(picp_batch_t* b, int world, int rank, picp_exchange_fn exchange,
+                                         void* user, int64_t n_total, float* T_all, picp_stats* st_all) {
+  CHECK_ARG(exchange && world >= 1 && rank >= 0 && rank < world && n_total >= 0,
+            "picp_batch_allgather_host: bad exchange or world/rank");
+  int rc = PICP_OK;
+  int64_t f0 = 0, f1 = 0;
+  const int64_t maxn = std::max<int64_t>(picp_shard_pad(n_total, world), 1);
+  constexpr size_t HDR = 16;
+  const size_t bytes = HDR + (size_t)maxn * sizeof(PicpState);
+  if (!b || !T_all) rc = set_err(PICP_ERR_ARG, "picp_batch_allgather_host: null argument");
+  else if ((rc = picp_shard_range(n_total, world, rank, &f0, &f1)) == PICP_OK && f1 - f0 != b->np)
+    rc = set_err(PICP_ERR_ARG, "picp_batch_allgather_host: the batch does not hold this rank's shard of n_total");
+  if (rc == PICP_OK && hipSetDevice(b->device) != hipSuccess)
+    rc = set_err(PICP_ERR_DEVICE, "picp_batch_allgather_host: hipSetDevice failed");
+  if (rc == PICP_OK) rc = batch_read_results(b);  // the solve is complete (re-run if a hand-off timed out)
+  const std::string local_err = rc ? picp_last_error() : "";
+  std::vector<char> send(bytes, 0), recv(bytes * (size_t)world, 0);
+  const int32_t status = rc;
+  memcpy(send.data(), &status, sizeof(status));
+  if (rc == PICP_OK) memcpy(send.data() + HDR, b->result_h.data(), (size_t)b->np * sizeof(PicpState));
+  const int xr = exchange(user, send.data(), recv.data(), bytes);
+  if (rc) return set_err(rc, "%s", local_err.c_str());
+  if (xr != 0) return set_err(PICP_ERR_STATE, "picp_batch_allgather_host: the exchange failed (%d)", xr);
+  std::vector<PicpState> padded((size_t)world * maxn), all((size_t)std::max<int64_t>(n_total, 1));
+  for (int r = 0; r < world; ++r) {
+    int32_t st = 0;
+    memcpy(&st, recv.data() + (size_t)r * bytes, sizeof(st));
+    if (st != PICP_OK)
+      return set_err(PICP_ERR_STATE, "picp_batch_allgather_host: rank %d failed before the exchange (%d)", r, st);
+    memcpy(padded.data() + (size_t)r * maxn, recv.data() + (size_t)r * bytes + HDR, (size_t)maxn * sizeof(PicpState));
   }
+  rc = picp_shard_unpack(n_total, world, sizeof(PicpState), padded.data(), all.data());
+  if (rc) return rc;
+  gather_to_poses(all.data(), n_total, T_all, st_all);
   return PICP_OK;
 }
 
@@ -1513,7 +1558,8 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   int64_t max_nr = 0;
   for (const MatchProblem& q : probs) max_nr = std::max(max_nr, q.nr);
   const int ks = picp_match_ksplit(n_problems, max_nq, max_nr, form);
-  const size_t b_part = ks > 1 ? (size_t)ks * n_problems * max_nq * sizeof(float4) : 0;
+  const int64_t part_cap = picp_match_split_scratch(ks, n_problems, max_nq);  // partials + tickets
+  const size_t b_part = (size_t)part_cap * sizeof(float4);
   char* buf = nullptr;
   HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + b_part + 512));
   char* cur = buf;
@@ -1535,12 +1581,13 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   hipError_t e = hipMemcpy(d_probs, probs.data(), b_probs, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_d1, desc1, b_d1, hipMemcpyHostToDevice);
   if (e == hipSuccess && n2) e = hipMemcpy(d_d2, desc2, (size_t)n2 * dim * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && d_part) e = hipMemset(d_part, 0, b_part);  // the split's tickets start at zero
   if (e == hipSuccess) e = picp_launch_match_prep(nullptr, d_d1, n1, dim, q_h, q_n1, q_n2);
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)
     e = picp_launch_match_mfma(nullptr, n_problems, max_nq, d_d1, d_d2, q_h, q_n1, r_h, r_n1, r_n2, d_probs,
                                dim, dist_thr, ratio_thr, d_bi, d_bd, d_sd, d_acc, form, ks, d_part,
-                               ks > 1 ? (int64_t)ks * n_problems * max_nq : 0);
+                               part_cap);
   if (e == hipSuccess) e = hipMemcpy(best_idx, d_bi, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(best_dist, d_bd, b_out, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(second_dist, d_sd, b_out, hipMemcpyDeviceToHost);

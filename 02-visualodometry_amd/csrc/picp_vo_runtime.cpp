@@ -237,9 +237,10 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
                     "VO schedule defaults to the serial order; concurrent schedules are not bit-stable with it\n");
   }
   if (const char* e = getenv("PICP_VO_OVERLAP")) h->overlap = atoi(e) != 0;
-  // at most two groups: three and four measured slower (C5 592k / 404k vs 597-600k frames/s with
-  // two, round 2)
-  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
+  // two groups by default: three and four measured slower at the throughput-bound default shape
+  // (C5 592k / 404k vs 597-600k frames/s with two, round 2); up to 8 for A/B at the
+  // latency-bound shapes (few segments per chain)
+  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(8, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
@@ -427,7 +428,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
     ks_w[c] = picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only, ks_force);
-    cap_w[c] = ks_w[c] > 1 ? (int64_t)ks_w[c] * nsc * h->max_obs : 0;
+    cap_w[c] = picp_match_split_scratch(ks_w[c], nsc, h->max_obs);  // partials + tickets (zeroed below)
     p_partw.push_back(part((size_t)cap_w[c] * sizeof(float4)));
   }
   // the frame->next launches, as vo_frame_match issues them: the whole table up front (overlap off)
@@ -440,7 +441,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
         const int n = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - q);
         const int k = picp_match_ksplit_forced(n, h->max_obs, h->max_obs, h->accept_only, ks_force);
         ks_p.emplace_back(q, k);
-        if (k > 1) cap_p = std::max(cap_p, (int64_t)k * n * h->max_obs);
+        cap_p = std::max(cap_p, picp_match_split_scratch(k, n, h->max_obs));
       }
     };
     const size_t nck = chunk_off.size() - 1;

@@ -46,7 +46,7 @@ EXPORTED = [
     "picp_vo_sync", "picp_vo_get_poses", "picp_vo_get_steps", "picp_vo_get_map", "picp_vo_time",
     "picp_vo_info", "picp_selftest_rcp", "picp_essential_params_default", "picp_essential_batch",
     "picp_shard_range", "picp_shard_pad", "picp_shard_unpack", "picp_comm_unique_id", "picp_comm_create", "picp_comm_destroy", "picp_comm_info",
-    "picp_comm_allreduce_max", "picp_comm_barrier", "picp_batch_allgather",
+    "picp_comm_allreduce_max", "picp_comm_barrier", "picp_batch_allgather", "picp_batch_allgather_host",
 ]
 COMM_ID_BYTES = 128
 
@@ -80,6 +80,8 @@ class Params(ctypes.Structure):
 
 
 _lib = None
+# picp_exchange_fn (include/picp_c.h): int (*)(void* user, const void* send, void* recv, size_t bytes)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
 
 def build():
@@ -162,6 +164,7 @@ def lib():
         "picp_comm_allreduce_max": ([vp, dp, i], i),
         "picp_comm_barrier": ([vp], i),
         "picp_batch_allgather": ([vp, vp, i64, fp, sp], i),
+        "picp_batch_allgather_host": ([vp, i, i, EXCHANGE_FN, vp, i64, fp, sp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -464,6 +467,34 @@ class Comm:
         st = (Stats * max(n_total, 1))()
         _check(lib().picp_batch_allgather(batch._b, self._c, n_total, _fptr(T), st))
         return np.transpose(T.reshape(n_total, 4, 4), (0, 2, 1)).copy(), [st[k].as_dict() for k in range(n_total)]
+
+
+def allgather_batch_host(batch, world, rank, n_total, exchange):
+    """picp_batch_allgather_host: the batch split's gather with the byte exchange done by the caller.
+    exchange(send: bytes) -> bytes of world * len(send), rank order (e.g. a gloo all_gather).
+    Returns every rank's poses (n_total, 4, 4) and stats dicts, like Comm.allgather_batch."""
+    err = []
+
+    def cb(user, send, recv, nbytes):
+        try:
+            out = exchange(ctypes.string_at(send, nbytes))
+            if len(out) != world * nbytes:
+                return 1
+            ctypes.memmove(recv, out, len(out))
+            return 0
+        except Exception as e:  # reported through the library's status, never across the C frame
+            err.append(e)
+            return 2
+
+    fn = EXCHANGE_FN(cb)
+    T = np.zeros(16 * max(n_total, 1), np.float32)
+    st = (Stats * max(n_total, 1))()
+    rc = lib().picp_batch_allgather_host(batch._b, world, rank, fn, None, n_total, _fptr(T), st)
+    if err:
+        raise err[0]
+    _check(rc)
+    return (np.transpose(T[:16 * n_total].reshape(n_total, 4, 4), (0, 2, 1)).copy(),
+            [st[k].as_dict() for k in range(n_total)])
 
 
 def projection_matrix(K, T_cw):

@@ -269,12 +269,14 @@ def _sub_short(d):
     """One sub-result (c3 / c4 / c5) in a few numbers."""
     if not d:
         return None
-    o = {"value": _r(d.get("value"), 5), "ms_per_step": _r(d.get("ms_per_step"), 5)}
+    o = {"value": _r(d.get("value"), 5)}
+    if "chain_step_us" not in d:  # a VO figure carries its chain step instead
+        o["ms_per_step"] = _r(d.get("ms_per_step"), 5)
     if d.get("roofline"):
         r = _roof_short(d["roofline"])
         o["roofline"] = {k: r[k] for k in ("bound", "frac", "kernel_us", "latency_frac", "issue_frac", "hbm_frac")
                          if k in r}
-    for k in ("chain_step_us", "pose_err_vs_gt_se3_max", "pose_err_vs_oracle_se3", "pose_err_vs_oracle_se3_frame0"):
+    for k in ("chain_step_us", "pose_err_vs_oracle_se3", "pose_err_vs_oracle_se3_frame0"):
         if k in d:
             o[k] = _r(d[k], 3)
     if "trajectory" in d:
@@ -290,11 +292,17 @@ def _sub_short(d):
         o["proj_eff_n8"] = d["projection_n8"]["efficiency"]
     if "per_rank_n8" in d:
         o["per_rank_n8"] = {"value": _r(d["per_rank_n8"]["value"]), "chain_step_us": d["per_rank_n8"].get("chain_step_us")}
-    if "partition_8e" in d:
-        q = d["partition_8e"]
-        o["partition_8e"] = {"value": _r(q["value"]), "chain_step_us": q.get("chain_step_us"),
-                             "ate_m": _r(q["trajectory"].get("ate_rmse_m", q["trajectory"].get("ate_rmse")), 4)
-                             if "trajectory" in q else None}
+    if "rounds_sync" in d:
+        o["rounds_sync"] = d["rounds_sync"]["ratio"]
+    if "essential_boot" in d:
+        q = d["essential_boot"]
+        o["essential_boot"] = {"value": _r(q["value"]), "ate_m": _r(q["trajectory"].get("ate_rmse_m"), 4),
+                               "rot_err_deg_max": _r(q["bootstrap"].get("rot_err_deg_max"), 3)}
+    if "gt_anchored_250" in d:
+        q = d["gt_anchored_250"]
+        o["gt_anchored_250"] = {"value": _r(q["value"]), "ate_m": _r(q["trajectory"].get("ate_rmse_m"), 4),
+                                "proj_eff_n8": q.get("projection_n8", {}).get("efficiency"),
+                                "per_rank_n8": _r(q["per_rank_n8"]["value"]) if "per_rank_n8" in q else None}
     return o
 
 
@@ -303,7 +311,7 @@ def compact_line(out, detail, sub_fields=False):
     in well under 2 KB (the driver keeps only the tail of stdout)."""
     line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                                 "higher_is_better", "scaling", "vs_baseline", "dtype") if k in out}
-    line["data"] = "synthetic (seeded, SURVEY §8d), resident in HBM"
+    line["data"] = "synthetic (seeded), resident in HBM"
     cfg = out.get("config", {})
     line["config"] = {k: cfg[k] for k in ("workload", "n_corr", "rounds", "frames", "segment_steps", "parallelism")
                       if k in cfg}
@@ -313,8 +321,8 @@ def compact_line(out, detail, sub_fields=False):
     if "cpu_baseline" in out:
         c = out["cpu_baseline"]
         line["cpu_baseline"] = {"value": _r(c["value"]), "unit": c["unit"], "cores": c["cores"], "kind": c["kind"],
-                                "sample": c["sample"].split(" (")[0]}
-    for k in ("pose_err_vs_oracle_se3", "pose_err_vs_gt_se3", "pose_err_vs_oracle_se3_frame0"):
+                                "sample": c["sample"].split(" of one")[0]}
+    for k in ("pose_err_vs_oracle_se3", "pose_err_vs_oracle_se3_frame0"):
         if k in out:
             line[k] = _r(out[k], 3)
     if "cpu_baseline_all_cores" in out:
@@ -573,26 +581,49 @@ def bench_frame(args, rk, torch):
             c3 = bench_frame(sub, rk, torch)
             c3["roofline"] = _resident_bound(c3["roofline"])
             out["c3"] = _compact(c3)
-        out["c5"] = _compact(bench_vo(sub, rk, torch))
-        # SURVEY.md §8e's partition: 8 contiguous segments over the sequence (one per GPU of an
-        # 8-GPU node), each bootstrapped once; here all 8 run on this rank's GPU(s)
+        # C5: SURVEY.md §8e's own partition leads -- 8 contiguous segments of
+        # 1,250 steps (one per GPU of an 8-GPU node; here all 8 on this rank's GPU(s)), each
+        # bootstrapped from its ground-truth pose pair; the same partition with the reference's
+        # two-view bootstrap (match_points + findEssentialMat/recoverPose, exec/icp_test.cpp:44-58)
+        # beside it; the 250 gt-anchored 40-step segments are a labelled side figure.
+        F = args.frames or WORKLOADS["c5"]["frames"]
+        L8 = -(-(F - 1) // 8)
         sub8 = argparse.Namespace(**vars(sub))
         sub8.steps, sub8.warmup, sub8.samples = 2, 1, 3
-        F = args.frames or WORKLOADS["c5"]["frames"]
+        c5_250 = bench_vo(sub, rk, torch)
         if rk.world <= 8:  # 8 segments: a world of more ranks would leave some with none
-            out["c5"]["partition_8e"] = _compact(bench_vo(sub8, rk, torch, seg_len=-(-(F - 1) // 8), tag="c5_8e"))
+            c5 = _compact(bench_vo(sub8, rk, torch, seg_len=L8, tag="c5_8e"))
+            ess = argparse.Namespace(**vars(sub8))
+            ess.c5_boot = "essential"
+            c5["essential_boot"] = _compact(bench_vo(ess, rk, torch, seg_len=L8, tag="c5_8e_ess"))
+        else:
+            c5 = {}
+        g = _compact(c5_250)
         if rk.world == 1:
-            # the per-rank shape of the default partition at N = 8 (rank 0's 32 of the 250
-            # segments), on this GPU alone: each rank still runs every segment's dependent steps
+            # the per-rank shapes at N = 8 on this GPU alone: the 8e partition's one segment per
+            # rank, and rank 0's 32 of the 250 segments
+            total8 = c5["value"] * c5["ms_per_step"] * 1e-3  # frames per run
+            n8 = bench_vo(sub8, rk, torch, seg_len=L8, shard=(8, 0), tag="c5_8e_n8")
+            c5["per_rank_n8"] = _compact(n8)
+            c5["projection_n8"] = {
+                "projected_value": round(total8 / (n8["ms_per_step"] * 1e-3), 1),
+                "efficiency": round(total8 / (n8["ms_per_step"] * 1e-3) / (8 * c5["value"]), 4),
+                "basis": "the 8 segments' frames / the time of rank 0's share (1 of 8 segments, 1,250 dependent "
+                         "steps) alone on one GPU"}
             n8 = bench_vo(sub, rk, torch, shard=(8, 0), tag="c5_n8")
-            total = out["c5"]["value"] * out["c5"]["ms_per_step"] * 1e-3  # frames per run
-            out["c5"]["per_rank_n8"] = _compact(n8)
-            out["c5"]["projection_n8"] = {
+            total = g["value"] * g["ms_per_step"] * 1e-3
+            g["per_rank_n8"] = _compact(n8)
+            g["projection_n8"] = {
                 "projected_value": round(total / (n8["ms_per_step"] * 1e-3), 1),
-                "efficiency": round(total / (n8["ms_per_step"] * 1e-3) / (8 * out["c5"]["value"]), 4),
+                "efficiency": round(total / (n8["ms_per_step"] * 1e-3) / (8 * g["value"]), 4),
                 "basis": "the whole sequence's frames / the time of rank 0's share (32 of 250 segments) alone on one "
                          "GPU: every rank still runs its segments' 40 dependent steps, so the time per run falls "
                          "with the width of each step, not with the step count"}
+        for k in ("cpu_baseline", "cpu_baseline_all_cores"):  # measured on the 40-step segments
+            if k in g:
+                c5[k] = g[k]
+        c5["gt_anchored_250"] = g
+        out["c5"] = c5
     return out
 
 
@@ -602,7 +633,7 @@ def _compact(d):
             "pose_err_vs_gt_se3", "pose_err_vs_gt_se3_max", "pose_err_vs_oracle_se3", "pose_err_vs_oracle_note",
             "pose_err_vs_oracle_se3_frame0", "trajectory", "chain_step_us", "per_rank", "projection",
             "kernel_us", "kernel", "traffic", "traffic_source",
-            "picp_iterations_per_s", "ranks", "config", "bootstrap")
+            "picp_iterations_per_s", "ranks", "config", "bootstrap", "rounds_sync")
     out = {k: d[k] for k in keep if k in d}
     if "config" in out:
         out["config"] = {k: v for k, v in out["config"].items()
@@ -841,12 +872,23 @@ def bench_vo(args, rk, torch, seg_len=None, shard=None, tag="c5"):
         boot = np.stack([[np.eye(4), e["T"]] for e in ess]).astype(np.float32)
         # unit baseline: the drift below is measured after scaling each segment to the ground
         # truth's first baseline (the reference's evaluation aligns scale the same way, umeyama)
+        rot_err, dir_err = [], []
         for k, f in enumerate(my_first):
-            scale[k] = np.linalg.norm((rel[k] @ D["T_cw"][f + 1])[:3, 3]) / max(np.linalg.norm(boot[k][1][:3, 3]), 1e-30)
+            gt1 = rel[k] @ D["T_cw"][f + 1]
+            scale[k] = np.linalg.norm(gt1[:3, 3]) / max(np.linalg.norm(boot[k][1][:3, 3]), 1e-30)
+            # the bootstrap's own error vs the ground-truth relative pose: rotation angle and the
+            # angle between the translation directions (the scale is not observable)
+            Rd = boot[k][1][:3, :3].astype(np.float64).T @ gt1[:3, :3]
+            rot_err.append(np.degrees(np.arccos(np.clip((np.trace(Rd) - 1.0) / 2.0, -1.0, 1.0))))
+            a, b = boot[k][1][:3, 3].astype(np.float64), gt1[:3, 3]
+            dir_err.append(np.degrees(np.arccos(np.clip(a @ b / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-300),
+                                                        -1.0, 1.0))))
         boot_info = {"kind": "essential: match_points + findEssentialMat(RANSAC) + recoverPose per segment on the "
                              "GPU (picp_match_points_batch, picp_essential_batch), unit baseline; before the timed "
                              "region", "ms": round(boot_ms, 3), "segments": len(my_first),
-                     "not_good": int(sum(1 for e in ess if not e["good"]))}
+                     "not_good": int(sum(1 for e in ess if not e["good"])),
+                     "rot_err_deg_max": float(np.max(rot_err)), "rot_err_deg_median": float(np.median(rot_err)),
+                     "t_dir_err_deg_max": float(np.max(dir_err)), "t_dir_err_deg_median": float(np.median(dir_err))}
     else:
         boot = np.stack([[np.eye(4), rel[k] @ D["T_cw"][f + 1]] for k, f in enumerate(my_first)]).astype(np.float32)
     vo = picp_amd.VOSequence(D["frame_off"], D["uv"], D["desc"], device=rk.device, K=seq.K)
@@ -869,6 +911,7 @@ def bench_vo(args, rk, torch, seg_len=None, shard=None, tag="c5"):
         rounds += int(Rr[k]["rounds"][1:].sum())
         corr += int((Rr[k]["rounds"][1:].astype(np.int64) * Rr[k]["n_corr"][1:]).sum())
     err = trk.max([err])[0]
+    sync = _rounds_sync([Rr[k]["rounds"][1:] for k in range(len(my_first))])
     tot = trk.gather_obj([rounds, corr, int(my_steps.sum())])
     rounds, corr, frames_total = (sum(t[i] for t in tot) for i in range(3))
     # the whole trajectory: every rank's segments (gathered to all ranks, after timing), stitched
@@ -919,6 +962,7 @@ def bench_vo(args, rk, torch, seg_len=None, shard=None, tag="c5"):
         "pose_err_frame": "camera-in-world poses in each segment's frame (its first camera)",
         "trajectory": traj,
         "bootstrap": boot_info,
+        "rounds_sync": sync,
     }
     if rk.world > 1 and sync_ranks:
         out["ranks"] = {"world_size_observed": rk.comm.world,
@@ -927,6 +971,27 @@ def bench_vo(args, rk, torch, seg_len=None, shard=None, tag="c5"):
         out["cpu_baseline"] = cpu_baseline_vo(seq, L, args.cpu_seconds)
         out["cpu_baseline_all_cores"] = cpu_baseline_vo_mt(seq, L, max(2.0, args.cpu_seconds / 2))
     return out
+
+
+def _rounds_sync(rounds, chains=2):
+    """What the per-step synchronisation of a VO run costs in PICP rounds.
+    Every step's PICP launch covers one chain's segments (the library's default: two contiguous
+    groups, picp_vo_runtime.cpp) and lasts as long as its slowest segment's rounds, so a chain pays
+    sum_t max_s rounds[s][t]; a segment alone would pay sum_t rounds[s][t].  ratio = the chains'
+    largest sum_t max_s over the largest single-segment sum: 1.0 means desynchronising the segments
+    cannot shorten the run (the slowest segment is slow at every step)."""
+    import numpy as np
+    n = len(rounds)
+    C = max(1, min(chains, n))
+    T = max(len(r) for r in rounds)
+    M = np.zeros((n, T), np.int64)
+    for k, r in enumerate(rounds):
+        M[k, :len(r)] = r
+    per_chain = [int(M[n * c // C:n * (c + 1) // C].max(0).sum()) for c in range(C)]
+    solo = int(M.sum(1).max())
+    return {"sum_t_max_s": max(per_chain), "max_s_sum_t": solo,
+            "ratio": round(max(per_chain) / max(solo, 1), 4), "mean_rounds": round(float(M[M > 0].mean()), 2),
+            "steps_at_50_any": int((M.max(0) >= 50).sum()), "steps": T, "chains": C}
 
 
 def _scaled(P, s):

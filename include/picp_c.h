@@ -201,6 +201,18 @@ int picp_comm_barrier(picp_comm_t* c);
  * leaving the others blocked in the collective. */
 int picp_batch_allgather(picp_batch_t* b, picp_comm_t* c, int64_t n_total, float* T_all,
                          picp_stats* st_all);
+/* The same gather with the byte exchange supplied by the caller instead of RCCL, for launchers
+ * whose ranks cannot form an RCCL communicator (several ranks on one GPU -- RCCL refuses a
+ * duplicate device -- or a CPU process group) and for testing the split at any world size.
+ * exchange(user, send, recv, bytes) must all-gather `bytes` from every rank's host buffer `send`
+ * into `recv` (world * bytes, rank order) and return 0.  One exchange per call: each rank sends
+ * a 16-byte header (its local status) and its shard's 128-byte states padded to
+ * picp_shard_pad(n_total, world) -- the layout picp_batch_allgather moves -- so a rank whose local
+ * checks failed makes every rank return an error after the one exchange.  A non-zero return of
+ * exchange is returned as PICP_ERR_STATE. */
+typedef int (*picp_exchange_fn)(void* user, const void* send, void* recv, size_t bytes);
+int picp_batch_allgather_host(picp_batch_t* b, int world, int rank, picp_exchange_fn exchange, void* user,
+                              int64_t n_total, float* T_all, picp_stats* st_all);
 
 /* ---------------- linear triangulation (cv::triangulatePoints replacement) ---------------- */
 
