@@ -21,7 +21,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
 extern "C" int picp_match_ksplit(int n_problems, int64_t max_nq, int64_t max_nr, int form);
 extern "C" int picp_match_ksplit_forced(int n_problems, int64_t max_nq, int64_t max_nr, int form, int force);
 extern "C" int picp_match_ksplit_env(void);
-// float4 of scratch (partials + arrival tickets, zeroed once by the owner) a split launch needs
+// float4 of scratch a split launch needs (the ranges' partials)
 extern "C" int64_t picp_match_split_scratch(int ksplit, int n_problems, int64_t max_nq);
 extern "C" int picp_match_prep_kch(int dim);
 

@@ -169,12 +169,6 @@ __host__ __device__ __forceinline__ int64_t mm_kchunk(int64_t nr, int ksplit) {
 __host__ __device__ __forceinline__ int mm_nsplit(int64_t nr, int ksplit) {
   return nr > 0 ? (int)((nr + mm_kchunk(nr, ksplit) - 1) / mm_kchunk(nr, ksplit)) : 0;
 }
-// A split launch's scratch (part): ksplit x n_problems x max_nq float4 partial top-2s, then one
-// arrival ticket per (problem, query block) -- n_problems x ceil(max_nq / 128) uint32, zero before
-// the first launch and re-zeroed by each ticket's last arriver (picp_match_split_scratch).
-__host__ __device__ __forceinline__ int64_t mm_part_words(int ksplit, int n_problems, int64_t max_nq) {
-  return (int64_t)ksplit * n_problems * max_nq;
-}
 #define MM_SAFE 60000.0f
 
 __device__ __forceinline__ float mm_bound(float nq, float rmax) {
@@ -397,20 +391,11 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     ks = blockIdx.x / gx;
   }
   MatchProblem P = probs[pid];
-  const MatchProblem P0 = P;  // the whole problem (P is narrowed to this block's range below)
   int64_t r_lo = 0;  // this block's references: [r_lo, r_lo + P.nr) of the problem's (P is local)
-  const int ns_all = (ksplit > 1) ? mm_nsplit(P.nr, ksplit) : 1;  // the problem's non-empty ranges
   if (ksplit > 1) {
-    if (P.nr == 0) {  // no reference at all: range 0's blocks store the empty scan's result
-      const int64_t qe = (int64_t)qblk * QPB + threadIdx.x;
-      if (ks == 0 && threadIdx.x < QPB && qe < P.nq)
-        match_store(P, P.q_off + qe, -1, FLT_MAX, FLT_MAX, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                    accepted);
-      return;
-    }
     const int64_t kc = mm_kchunk(P.nr, ksplit);
     r_lo = (int64_t)ks * kc;
-    if (r_lo >= P.nr) return;  // an empty range (the tickets count only mm_nsplit ranges)
+    if (r_lo >= P.nr) return;  // an empty range (the merge reads only mm_nsplit ranges)
     P.r_off += r_lo;
     P.nr = min(kc, P.nr - r_lo);
   }
@@ -828,74 +813,46 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
       }
     }
-    if (ksplit > 1) {  // this range's top-2 (global index), merged in range order below
-      // two write-through 8-byte words (relaxed agent-scope stores: sc1), read back with sc1 loads
-      unsigned long long* pw = reinterpret_cast<unsigned long long*>(part + ((int64_t)ks * n_problems + pid) * part_nq + qi);
-      const int32_t gbi = bi >= 0 ? (int32_t)(bi + r_lo) : -1;
-      __hip_atomic_store(pw, ((unsigned long long)__float_as_uint(best) << 32) | (unsigned)gbi, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(pw + 1, (unsigned long long)__float_as_uint(second), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    } else {
+    if (ksplit > 1)  // this range's top-2 (global index), merged in range order by picp_match_merge_kernel
+      part[((int64_t)ks * n_problems + pid) * part_nq + qi] =
+          make_float4(__int_as_float(bi >= 0 ? (int32_t)(bi + r_lo) : -1), best, second, 0.0f);
+    else
       match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
                   accepted);  // :100-103
+  }
+}
+
+// The reference ranges of a split launch, merged in index order: the reference's in-order
+// strict-'<' scan over range 0, then range 1, ... yields best = the smaller best (a tie keeps the
+// earlier range's, i.e. the lower index), second = the second smallest of the union.  Each range's
+// (best, first index, second) is exactly its own in-order scan's (index-order-independent update
+// above), so the merged triple is the whole scan's.  One thread per query.
+extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, int n_problems,
+                                                   int ksplit, const float4* __restrict__ part, int64_t part_nq,
+                                                   float dist_thr, float ratio_thr, int32_t* __restrict__ best_idx,
+                                                   float* __restrict__ best_dist, float* __restrict__ second_dist,
+                                                   int32_t* __restrict__ accepted) {
+  const int pid = blockIdx.y;
+  const MatchProblem P = probs[pid];
+  const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= P.nq) return;
+  const int ns = mm_nsplit(P.nr, ksplit);
+  float best = FLT_MAX, second = FLT_MAX;  // src/my_utilities.h:78-79
+  int32_t bi = -1;
+  for (int k = 0; k < ns; ++k) {
+    const float4 r = part[((int64_t)k * n_problems + pid) * part_nq + qi];
+    const float b = r.y;
+    if (b < best) {
+      second = fminf(best, r.z);
+      best = b;
+      bi = __float_as_int(r.x);
+    } else if (b == best) {
+      second = best;  // two equal values in the multiset; the earlier index stays
+    } else {
+      second = fminf(second, b);
     }
   }
-  if (ksplit <= 1) return;
-  // ---------------- the reference ranges merged by the last of them to finish ----------------
-  // The in-launch split-K combine (cdna_hip_programming.md §6 Guideline 16, as picp_round_kernel's
-  // last arriver): every wave drains its partial stores, then the block takes its (problem, query
-  // block) ticket; the block that takes the last of the problem's mm_nsplit tickets merges.
-  // Saves the separate merge launch on the VO world match's chain (round 5: 5-8 us per step).
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  unsigned* tickets = reinterpret_cast<unsigned*>(part + mm_part_words(ksplit, n_problems, part_nq));
-  unsigned* tk = tickets + (int64_t)pid * gx + qblk;
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (old == (unsigned)(ns_all - 1)) ? 1 : 0;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
-  const int64_t qm = q0 + tid;
-  if (tid < QPB && qm < P.nq) {
-    // src/my_utilities.h:78-99 over range 0, then range 1, ...: best = the smaller best (a tie
-    // keeps the earlier range's, i.e. the lower index), second = the second smallest of the union.
-    // Each range's (best, first index, second) is its own in-order scan's, so the merged triple is
-    // the whole scan's.
-    unsigned long long w0[MM_KSPLIT_MAX], w1[MM_KSPLIT_MAX];
-    float best = FLT_MAX, second = FLT_MAX;
-    int32_t bi = -1;
-    for (int k0 = 0; k0 < ns_all; k0 += MM_KSPLIT_MAX) {  // every load of a chunk before the first use
-      const int kn = min(MM_KSPLIT_MAX, ns_all - k0);
-#pragma unroll
-      for (int u = 0; u < MM_KSPLIT_MAX; ++u)
-        if (u < kn) {
-          const unsigned long long* pw =
-              reinterpret_cast<const unsigned long long*>(part + ((int64_t)(k0 + u) * n_problems + pid) * part_nq + qm);
-          w0[u] = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          w1[u] = __hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-      for (int u = 0; u < MM_KSPLIT_MAX; ++u)
-        if (u < kn) {
-          const float b = __uint_as_float((unsigned)(w0[u] >> 32)), sc = __uint_as_float((unsigned)w1[u]);
-          if (b < best) {
-            second = fminf(best, sc);
-            best = b;
-            bi = (int32_t)(unsigned)w0[u];
-          } else if (b == best) {
-            second = best;  // two equal values in the multiset; the earlier index stays
-          } else {
-            second = fminf(second, b);
-          }
-        }
-    }
-    match_store(P0, P0.q_off + qm, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                accepted);  // :100-103
-  }
+  match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted);
 }
 
 extern "C" int picp_match_prep_kch(int dim) { return dim <= 16 ? 1 : 2; }
@@ -909,8 +866,6 @@ extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* de
                      stream, desc, n, dim, picp_match_prep_kch(dim), h, n1, n2);
   return hipGetLastError();
 }
-
-extern "C" int64_t picp_match_split_scratch(int ksplit, int n_problems, int64_t max_nq);
 
 // The pre-filtered match over prepped descriptors (picp_launch_match_prep).  form (include/picp_c.h
 // PICP_MATCH_FORM_*): bit 0 = the accept-only radius form (only accepted[] and the best index of
@@ -927,7 +882,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
   // part_cap: the scratch's capacity in float4; a split launch writes ksplit x n_problems x max_nq
   if (ksplit < 1 || ksplit > MM_KSPLIT_LIMIT) return hipErrorInvalidValue;
-  if (ksplit > 1 && (!part || picp_match_split_scratch(ksplit, n_problems, max_nq) > part_cap)) return hipErrorInvalidValue;
+  if (ksplit > 1 && (!part || (int64_t)ksplit * n_problems * max_nq > part_cap)) return hipErrorInvalidValue;
   const bool accept_only = (form & 1) != 0;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
   // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
@@ -981,6 +936,13 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   }
 #undef PICP_LAUNCH_MM3
 #undef PICP_LAUNCH_MM
+  if (ksplit > 1) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(picp_match_merge_kernel, dim3((unsigned)((max_nq + 255) / 256), (unsigned)n_problems),
+                       dim3(256), 0, stream, probs, n_problems, ksplit, (const float4*)part, part_nq, dist_thr,
+                       ratio_thr, best_idx, best_dist, second_dist, accepted);
+  }
   return hipGetLastError();
 }
 
@@ -1011,12 +973,12 @@ extern "C" int picp_match_ksplit_forced(int n_problems, int64_t max_nq, int64_t 
   return (int)std::min<int64_t>(std::max<int64_t>(k, k_range), MM_KSPLIT_LIMIT);
 }
 
-// float4 of scratch a split launch needs: the partials, then the tickets (at the smallest query
-// block, 128 queries, so either RB fits)
+// float4 of scratch a split launch needs: the ranges' partial top-2s (picp_match_merge_kernel
+// merges them).  Round 6 measured a fused form (the last-arriving range block merges, arrival
+// tickets behind the partials; commit 069e837) slower at every C5 shape: 8e 42.7k-42.9k vs
+// 41.9k frames/s, the N = 8 per-rank shape 162.3k vs 156.3k (profiles/r06/t2/ab.log).
 extern "C" int64_t picp_match_split_scratch(int ksplit, int n_problems, int64_t max_nq) {
-  if (ksplit <= 1) return 0;
-  const int64_t gx_max = (max_nq + 32 * MM_WAVES - 1) / (32 * MM_WAVES);
-  return mm_part_words(ksplit, n_problems, max_nq) + ((int64_t)n_problems * gx_max + 3) / 4;
+  return ksplit > 1 ? (int64_t)ksplit * n_problems * max_nq : 0;
 }
 
 extern "C" int picp_match_ksplit_env(void) {

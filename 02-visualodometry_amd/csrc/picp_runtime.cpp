@@ -1558,7 +1558,7 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   int64_t max_nr = 0;
   for (const MatchProblem& q : probs) max_nr = std::max(max_nr, q.nr);
   const int ks = picp_match_ksplit(n_problems, max_nq, max_nr, form);
-  const int64_t part_cap = picp_match_split_scratch(ks, n_problems, max_nq);  // partials + tickets
+  const int64_t part_cap = picp_match_split_scratch(ks, n_problems, max_nq);
   const size_t b_part = (size_t)part_cap * sizeof(float4);
   char* buf = nullptr;
   HIP_TRY(hipMalloc(&buf, b_probs + b_d1 + b_d2 + 4 * b_out + b_prep + b_part + 512));
@@ -1581,7 +1581,6 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   hipError_t e = hipMemcpy(d_probs, probs.data(), b_probs, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_d1, desc1, b_d1, hipMemcpyHostToDevice);
   if (e == hipSuccess && n2) e = hipMemcpy(d_d2, desc2, (size_t)n2 * dim * sizeof(float), hipMemcpyHostToDevice);
-  if (e == hipSuccess && d_part) e = hipMemset(d_part, 0, b_part);  // the split's tickets start at zero
   if (e == hipSuccess) e = picp_launch_match_prep(nullptr, d_d1, n1, dim, q_h, q_n1, q_n2);
   if (e == hipSuccess && n2) e = picp_launch_match_prep(nullptr, d_d2, n2, dim, r_h, r_n1, r_n2);
   if (e == hipSuccess)

@@ -66,14 +66,6 @@ __device__ __forceinline__ int vo_block_rank(bool flag, int* s_cnt, int* total) 
 // pair order), triangulate them with (previous pose, new pose) and append (xyz, curr descriptor)
 // to the map (pass 2), then write the next step's world-match problem and PICP initial state.
 // st_res: the PICP result (a.st_out[s]); n_corr: the PICP input size (a.probs[s].n).  Contains barriers: every thread calls.
-// The kernel is one latency chain per segment, so its global round trips are ordered to overlap:
-// pass 1's match loads are issued before thread 0's pose prologue (they depend only on the
-// frame offsets), the selected pairs stay in LDS (VO_APPEND_LDS_PAIRS of them; a larger frame's
-// tail goes through the segment's global pairs buffer), and pass 2 issues every load of a pair --
-// pixels, descriptor row, prepped row, norms -- before its triangulation.
-#ifndef VO_APPEND_LDS_PAIRS
-#define VO_APPEND_LDS_PAIRS 4096
-#endif
 template <int NT>
 __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, const PicpState* st_res, int n_corr) {
   constexpr int NW = NT / 64;
@@ -85,20 +77,10 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
   __shared__ float sTn[16];
   __shared__ int64_t s_base;
   __shared__ int s_cnt[NW];
-  __shared__ int2 s_pairs[VO_APPEND_LDS_PAIRS];
   const int64_t cf = G.f0 + (boot ? 0 : t), nf = cf + 1;
   const int64_t oc = a.frame_off[cf], nc = a.frame_off[cf + 1] - oc;
   const int64_t on = a.frame_off[nf];
   const int64_t rec = G.slot0 + (boot ? 0 : t + 1);
-  // pass 1's loads first (accept flag and next index; the next point's map match after them) ...
-  bool fl[PF];
-  int jb[PF];
-#pragma unroll
-  for (int c = 0; c < PF; ++c) {
-    const int64_t i = (int64_t)c * NT + threadIdx.x;
-    fl[c] = i < nc && a.pm_acc[oc + i] != 0;
-    jb[c] = (i < nc) ? a.pm_bi[oc + i] : 0;
-  }
   if (threadIdx.x == 0) {
     float Tp[16], Te[16];
     if (boot) {
@@ -111,7 +93,6 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
       for (int k = 0; k < 16; ++k) a.poses[16 * G.slot0 + k] = Tp[k];  // poses = {T0}
       s_base = 0;
     } else {
-      const int64_t mn = a.map_n[s];
 #pragma unroll
       for (int k = 0; k < 16; ++k) Tp[k] = a.poses[16 * (G.slot0 + t) + k];
       const PicpState st = *st_res;
@@ -137,7 +118,7 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
       r.converged = st.converged;
       r.n_proj = st.n_proj;
       a.steps[rec] = r;
-      s_base = mn;
+      s_base = a.map_n[s];
     }
     float Kl[9];
 #pragma unroll
@@ -148,26 +129,31 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
 #pragma unroll
     for (int k = 0; k < 16; ++k) sTn[k] = boot ? Tp[k] : Te[k];
   }
-#pragma unroll
-  for (int c = 0; c < PF; ++c)  // ... next point not among the map correspondences
-    fl[c] = fl[c] && (boot || a.wm_acc[on + (fl[c] ? jb[c] : 0)] == 0);
   __syncthreads();
   const int64_t mbase = G.map_off + s_base;
   const int dim = a.dim;
-  int2* pairs = a.pairs + (int64_t)s * a.cap_c;  // pairs past VO_APPEND_LDS_PAIRS
-  auto put = [&](int64_t k, int2 v) {
-    if (k < VO_APPEND_LDS_PAIRS) s_pairs[k] = v;
-    else pairs[k] = v;
-  };
-  // pass 1: the selected (curr, next) pairs in pair order (add_new_world_points), ordered
-  // compaction from registers
+  int2* pairs = a.pairs + (int64_t)s * a.cap_c;
+  // pass 1: the selected (curr, next) pairs in pair order (add_new_world_points)
   int64_t cnt = 0;
+  // every chunk's loads first (accept flag and next index, then the next point's map match), ...
+  bool fl[PF];
+  int jb[PF];
+#pragma unroll
+  for (int c = 0; c < PF; ++c) {
+    const int64_t i = (int64_t)c * NT + threadIdx.x;
+    fl[c] = i < nc && a.pm_acc[oc + i] != 0;
+    jb[c] = (i < nc) ? a.pm_bi[oc + i] : 0;
+  }
+#pragma unroll
+  for (int c = 0; c < PF; ++c)  // next point not among the map correspondences
+    fl[c] = fl[c] && (boot || a.wm_acc[on + (fl[c] ? jb[c] : 0)] == 0);
+  // ... then the ordered compaction from registers
 #pragma unroll
   for (int c = 0; c < PF; ++c) {
     if ((int64_t)c * NT >= nc) break;  // uniform
     int tot;
     const int r = vo_block_rank<NW>(fl[c], s_cnt, &tot);
-    if (fl[c]) put(cnt + r, make_int2(c * NT + (int)threadIdx.x, jb[c]));
+    if (fl[c]) pairs[cnt + r] = make_int2(c * NT + (int)threadIdx.x, jb[c]);
     cnt += tot;
   }
   for (int64_t c0 = (int64_t)PF * NT; c0 < nc; c0 += NT) {  // frames > 4096 obs
@@ -180,18 +166,19 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
     }
     int tot;
     const int r = vo_block_rank<NW>(flag, s_cnt, &tot);
-    if (flag) put(cnt + r, make_int2((int)i, j));
+    if (flag) pairs[cnt + r] = make_int2((int)i, j);
     cnt += tot;
   }
   __syncthreads();
   // pass 2: every lane triangulates (src/cam.cpp:115-139) and appends (xyz, curr descriptor)
   for (int64_t k = threadIdx.x; k < cnt; k += NT) {
-    const int2 pr = (k < VO_APPEND_LDS_PAIRS) ? s_pairs[k] : pairs[k];
+    const int2 pr = pairs[k];
     const int64_t slot = mbase + k;
-    // every load of the pair before the triangulation's FP64 chain: the descriptor row and the
-    // matcher's prepped row of it (fp16 + guard norms) do not depend on it, and the stores come
-    // after (the compiler cannot rule out that a store aliases a later load)
-    const float2 u1 = a.uv[oc + pr.x], u2 = a.uv[on + pr.y];
+    float o[3];
+    triangulate_dlt(sP, sP + 12, a.uv[oc + pr.x], a.uv[on + pr.y], o);
+    // the descriptor row and the matcher's prepped row of it (fp16 + guard norms): every load
+    // first, then the stores -- the compiler cannot rule out that a store aliases a later load,
+    // so an interleaved element copy paid one global round trip per element
     const int64_t src = oc + pr.x;
     float dv[32];  // dim <= 32 (picp_vo_create)
 #pragma unroll
@@ -201,8 +188,6 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
 #pragma unroll
     for (int c = 0; c < 4; ++c) hv[c] = (c < a.dp / 8) ? hs[c] : make_uint4(0u, 0u, 0u, 0u);
     const float n1 = a.obs_n1[src], n2 = a.obs_n2[src];
-    float o[3];
-    triangulate_dlt(sP, sP + 12, u1, u2, o);
     a.map_xyz[3 * slot + 0] = o[0];
     a.map_xyz[3 * slot + 1] = o[1];
     a.map_xyz[3 * slot + 2] = o[2];

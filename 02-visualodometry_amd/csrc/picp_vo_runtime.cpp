@@ -237,10 +237,12 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
                     "VO schedule defaults to the serial order; concurrent schedules are not bit-stable with it\n");
   }
   if (const char* e = getenv("PICP_VO_OVERLAP")) h->overlap = atoi(e) != 0;
-  // two groups by default: three and four measured slower at the throughput-bound default shape
-  // (C5 592k / 404k vs 597-600k frames/s with two, round 2); up to 8 for A/B at the
-  // latency-bound shapes (few segments per chain)
-  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(8, atoi(e)));
+  // at most two groups: three and four measured slower at the default shape (C5 592k / 404k vs
+  // 597-600k frames/s with two, round 2), and so did four and eight at the
+  // latency-bound shapes, where a step waits for its chain's slowest segment (round 6: 8e
+  // 32.5k / 18.4k vs 42.0k frames/s, the N = 8 per-rank shape 90.2k / 50.0k vs 156.9k;
+  // profiles/r06/t2/ab.log): the chains share 4 hardware queues
+  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
@@ -428,7 +430,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
     ks_w[c] = picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only, ks_force);
-    cap_w[c] = picp_match_split_scratch(ks_w[c], nsc, h->max_obs);  // partials + tickets (zeroed below)
+    cap_w[c] = picp_match_split_scratch(ks_w[c], nsc, h->max_obs);
     p_partw.push_back(part((size_t)cap_w[c] * sizeof(float4)));
   }
   // the frame->next launches, as vo_frame_match issues them: the whole table up front (overlap off)

@@ -15,7 +15,9 @@ segments (a few thousand map rows); this file covers the long form at its full s
       float32 arithmetic summing in three orders).  The rule:
         (1) SE(3) log < 1e-4 (north_star) against the reference's own arithmetic in its own order
             (FAITHFUL: sequential float sums, src/picp_solver.cpp:56-105), camera-in-world;
-        (2) against EVERY restatement, in both pose bases (camera-in-world, the trajectory's form;
+        (2) against EVERY restatement (the four above and two in the GPU's own arithmetic class:
+            float64 sums, float32 H, a float32 or float64 solve), in both pose bases
+            (camera-in-world, the trajectory's form;
             world-in-camera, the next step's prior), SE(3) log < max(1e-4, 2 x cloud), where the
             cloud is the largest distance between two restatements in that basis: what float
             rounding alone does to this step's pose.  Late in a long segment the f64-vs-float32
@@ -58,6 +60,27 @@ def _iso_inverse_f32(T):
         s = np.float32(s + np.float32(R[2, i] * t[2]))
         out[i, 3] = -s
     return out
+
+
+def _mixed_solve(oracle, T0, K, world, img, pairs, rounds, f32_solve):
+    """The GPU's arithmetic class as a restatement: each round's H and b summed in float64 from the
+    float32 per-correspondence terms (oracle MODE_F64 linearize, src/picp_solver.cpp:56-91), rounded
+    to float32 with the damping added (:96), then solved in float32 by the Eigen-LDLT restatement
+    (f32_solve) or in float64 from those float32 values, and T <- v2tEuler(dx) * T in float32
+    (:102-103).  The oracle's two modes vary the summation only (FAITHFUL: float32 sums and solve,
+    F64: float64 sums and solve); these two vary the solve's precision around float64 sums, which
+    is what the GPU does (double partials, float32 LDL^T)."""
+    T = np.asarray(T0, np.float32).copy()
+    for _ in range(rounds):
+        lin = oracle.linearize(T, K, 480, 640, world, img, pairs, THR, mode=oracle.MODE_F64)
+        H = (np.asarray(lin["H"], np.float64) + np.eye(6)).astype(np.float32)
+        b = np.asarray(lin["b"], np.float64).astype(np.float32)
+        if f32_solve:
+            dx = np.asarray(oracle.ldlt_solve6(H, -b, double=False), np.float32)
+        else:
+            dx = np.linalg.solve(H.astype(np.float64), -b.astype(np.float64)).astype(np.float32)
+        T = (oracle.v2t_euler(dx).astype(np.float32) @ T).astype(np.float32)
+    return T
 
 
 def _cw_dist(T, P):
@@ -124,8 +147,13 @@ def test_vo_8e_segment_teacher_forced_late_steps(oracle, segment_8e, t):
     # The round count is then teacher-forced too: the oracle runs exactly the GPU's rounds, in
     # float64 accumulation and in the reference's float32 arithmetic (FAITHFUL: sequential float
     # sums, float LDL^T) with the correspondences in their order, reversed and in a seeded random
-    # order.  Every one of them is a correct restatement; their spread (the "cloud") is what float
-    # rounding alone does to this step's pose, printed beside the GPU's distance to each.
+    # order, and in the GPU's arithmetic class (float64 sums, float32 H, the solve in float32 or
+    # float64: _mixed_solve).  Every one of them is a correct restatement; their spread (the
+    # "cloud") is what float rounding alone does to this step's pose, printed beside the GPU's
+    # distance to each.  (Measured on the round-6 dump: in world-in-camera form the summation-order
+    # variants alone spread 1.8e-4 at step 1,249 while the solve-precision variants move the pose by
+    # up to 5e-4 at step 800 -- the 28 m lever arm on a 1e-5 rotation -- so a cloud of summation
+    # orders alone under-states float rounding there; profiles/r06/parity/.)
     variants = {}
     for name, mode, order in (("f64", oracle.MODE_F64, None), ("faithful", oracle.MODE_FAITHFUL, None),
                               ("faithful-rev", oracle.MODE_FAITHFUL, np.arange(len(pairs))[::-1]),
@@ -133,6 +161,8 @@ def test_vo_8e_segment_teacher_forced_late_steps(oracle, segment_8e, t):
         pp = pairs if order is None else np.ascontiguousarray(pairs[order])
         variants[name], _ = oracle.solve(T0, K, 480, 640, mx[:m], img, pp, THR, max_rounds=gr, conv_eps=-1.0,
                                          mode=mode)
+    variants["f64sum-f32solve"] = _mixed_solve(oracle, T0, K, mx[:m], img, pairs, gr, True)
+    variants["f64sum-f64solve"] = _mixed_solve(oracle, T0, K, mx[:m], img, pairs, gr, False)
     gpu_to = {k: _cw_dist(v, P[t + 1]) for k, v in variants.items()}
     names = list(variants)
     cloud = max(se3_log_norm(_iso_inverse_f32(variants[a]), _iso_inverse_f32(variants[b]))
