@@ -966,8 +966,8 @@ extern "C" int picp_match_ksplit_forced(int n_problems, int64_t max_nq, int64_t 
   }
   const int64_t base = (int64_t)n_problems * ((max_nq + 32 * MM_WAVES - 1) / (32 * MM_WAVES));
   int64_t k = (4 * (int64_t)num_cu + base - 1) / std::max<int64_t>(base, 1);
-  if (force > 0) k = force;
   k = std::max<int64_t>(1, std::min<int64_t>(k, MM_KSPLIT_MAX));
+  if (force > 0) k = std::min<int64_t>(force, MM_KSPLIT_LIMIT);  // an A/B count may pass the cap
   // the entries' range: split the largest set at least that far (beyond the occupancy cap)
   const int64_t k_range = (max_nr + ((int64_t)MM_RT << 12) - 1) / ((int64_t)MM_RT << 12);
   return (int)std::min<int64_t>(std::max<int64_t>(k, k_range), MM_KSPLIT_LIMIT);
