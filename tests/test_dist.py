@@ -146,3 +146,56 @@ def test_bench_launcher_one_failing_rank_ends_the_job():
                        capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode != 0, (r.returncode, r.stderr[-2000:])
     assert time.time() - t0 < 200
+
+
+def _host_exchange_null_worker(rank, world, port, q):
+    import ctypes
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "02-visualodometry_amd"))
+    import torch
+    import torch.distributed as dist
+    import picp_amd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def exchange(buf):
+        calls.append(len(buf))
+        t = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return b"".join(o.numpy().tobytes() for o in out)
+
+    class NoBatch:  # a rank with no batch: its local check fails
+        _b = ctypes.c_void_p()
+
+    try:
+        picp_amd.allgather_batch_host(NoBatch(), world, rank, 5, exchange)
+        q.put((rank, "no error", calls))
+    except picp_amd.PicpError as e:
+        q.put((rank, str(e), calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_host_exchange_gather_failure_needs_no_second_collective():
+    """picp_batch_allgather_host (CPU, gloo world 2, no device): a rank whose local check fails
+    (here: no batch at all) still takes part in the ONE exchange -- its status header travels in
+    it -- and returns an error; no rank waits in a collective the other never enters.  The GPU
+    suite runs the successful gather at world 2 and 3 (tests/test_gpu_dist.py)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_exchange_null_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=240) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, msg, calls in got:
+        assert "null argument" in msg, (rank, msg)
+        # one exchange of a 16-byte header + ceil(5 / 2) = 3 padded 128-byte states
+        assert calls == [16 + 3 * 128], (rank, calls)
