@@ -827,7 +827,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 // earlier range's, i.e. the lower index), second = the second smallest of the union.  Each range's
 // (best, first index, second) is exactly its own in-order scan's (index-order-independent update
 // above), so the merged triple is the whole scan's.  One thread per query.
-extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, int n_problems,
+template <int MM_MERGE_CHUNK>
+__global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, int n_problems,
                                                    int ksplit, const float4* __restrict__ part, int64_t part_nq,
                                                    float dist_thr, float ratio_thr, int32_t* __restrict__ best_idx,
                                                    float* __restrict__ best_dist, float* __restrict__ second_dist,
@@ -839,17 +840,29 @@ extern "C" __global__ void picp_match_merge_kernel(const MatchProblem* __restric
   const int ns = mm_nsplit(P.nr, ksplit);
   float best = FLT_MAX, second = FLT_MAX;  // src/my_utilities.h:78-79
   int32_t bi = -1;
-  for (int k = 0; k < ns; ++k) {
-    const float4 r = part[((int64_t)k * n_problems + pid) * part_nq + qi];
-    const float b = r.y;
-    if (b < best) {
-      second = fminf(best, r.z);
-      best = b;
-      bi = __float_as_int(r.x);
-    } else if (b == best) {
-      second = best;  // two equal values in the multiset; the earlier index stays
-    } else {
-      second = fminf(second, b);
+  // the ranges in chunks of MM_MERGE_CHUNK (4 or 16: the launch's ksplit rounded up), every load of a
+  // chunk issued before the first use: the kernel is one short latency chain on the VO world
+  // match's path (8e partition: 187 -> 181 us per step with 16, profiles/r06/t4/ab.log)
+  for (int k0 = 0; k0 < ns; k0 += MM_MERGE_CHUNK) {
+    float4 rr[MM_MERGE_CHUNK];
+#pragma unroll
+    for (int u = 0; u < MM_MERGE_CHUNK; ++u)  // unconditional (clamped) loads: no branch between them
+      rr[u] = part[((int64_t)min(k0 + u, ns - 1) * n_problems + pid) * part_nq + qi];
+#pragma unroll
+    for (int u = 0; u < MM_MERGE_CHUNK; ++u) {
+      const float4 r = rr[u];
+      // a range past ns contributes +inf: never below best or equal to it, and fminf(second, inf)
+      // leaves second -- a no-op
+      const float b = (k0 + u < ns) ? r.y : INFINITY;
+      if (b < best) {
+        second = fminf(best, r.z);
+        best = b;
+        bi = __float_as_int(r.x);
+      } else if (b == best) {
+        second = best;  // two equal values in the multiset; the earlier index stays
+      } else {
+        second = fminf(second, b);
+      }
     }
   }
   match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted);
@@ -905,7 +918,10 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   }
   const int64_t blocks_rb2 = (int64_t)n_problems * ((max_nq + 2 * 32 * MM_WAVES - 1) / (2 * 32 * MM_WAVES));
   // (measured for the folded accept-only form only; the others need 130-224 VGPRs at RB = 2)
-  int rb = (fold && blocks_rb2 >= 4 * (int64_t)num_cu) ? 2 : 1;
+  // ... or when an occupancy split of 8+ ranges already multiplies the grid (few problems against
+  // long reference sets: the 8e world match, 43.9k -> 44.8k frames/s; at the per-rank shape's 4
+  // ranges RB = 2 measured 2.4 % slower; profiles/r06/t3/ab.log)
+  int rb = (fold && (blocks_rb2 >= 4 * (int64_t)num_cu || ksplit >= 8)) ? 2 : 1;
   if (const char* e = getenv("PICP_MATCH_RB")) rb = (atoi(e) == 2) ? 2 : 1;
   const int qpb = MM_WAVES * 32 * rb;
   const int gx = (int)((max_nq + qpb - 1) / qpb);
@@ -939,9 +955,15 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   if (ksplit > 1) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(picp_match_merge_kernel, dim3((unsigned)((max_nq + 255) / 256), (unsigned)n_problems),
-                       dim3(256), 0, stream, probs, n_problems, ksplit, (const float4*)part, part_nq, dist_thr,
-                       ratio_thr, best_idx, best_dist, second_dist, accepted);
+    const dim3 mg((unsigned)((max_nq + 255) / 256), (unsigned)n_problems);
+    if (ksplit <= 4)
+      hipLaunchKernelGGL(picp_match_merge_kernel<4>, mg, dim3(256), 0, stream, probs, n_problems, ksplit,
+                         (const float4*)part, part_nq, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                         accepted);
+    else
+      hipLaunchKernelGGL(picp_match_merge_kernel<16>, mg, dim3(256), 0, stream, probs, n_problems, ksplit,
+                         (const float4*)part, part_nq, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+                         accepted);
   }
   return hipGetLastError();
 }

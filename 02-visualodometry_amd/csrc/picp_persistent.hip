@@ -67,11 +67,10 @@ typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #endif
 // each solver owns two pose sets (its L2 copy and its agent-scope copy) of the problem's region
 static_assert(2 * PICP_PSOLVERS <= PICP_POSE_SETS, "PICP_PSOLVERS needs 2 pose sets each (picp_internal.h)");
-// A solver whose sweep is still incomplete after this many passes also checks the error word, so a
-// timeout in another solver (whose followers then stop publishing) ends this one's wait in the same
-// round instead of at its own deadline.  Rounds complete within a few passes, so the check is off
-// every path that finishes.
-#define PICP_SWEEP_ERR_PASSES 32
+// (A timeout in one solver ends its followers' waits; the other solvers then wait out their own
+// deadline before the error word forces the re-run.  Checking the error word every 32 passes of an
+// incomplete sweep would end them sooner, but that check in the spin loops measured C2 -2.6 %,
+// C3 -1.2 % on the normal path (profiles/r06/t4/ab.log), so timeouts keep the two-window cost.)
 // raw buffer load aux: sc1 (bit 4: bypass L1, served by L2 / the fabric) | volatile (bit 31:
 // never hoisted out of a spin loop)
 #define PICP_AUX_SC1_VOLATILE ((int)(16u | 0x80000000u))
@@ -304,7 +303,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
         __builtin_amdgcn_s_sleep(SWEEP_ST);
         wb = pending;
         issue(gb, wb);
-        for (int it = 1;; ++it) {
+        for (;;) {
           take(ga, wa);
           if (!pending) break;
           wa = pending;
@@ -316,10 +315,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           if (timed_out(deadline)) {
             __hip_atomic_store(errw, 1u, RLX_AGENT);
             s_tmo = 1;
-            break;
-          }
-          if ((it % (PICP_SWEEP_ERR_PASSES / 2)) == 0 && __hip_atomic_load(errw, RLX_AGENT) != 0u) {
-            s_tmo = 1;  // another block timed out: its partials may never come
             break;
           }
         }
@@ -341,10 +336,6 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
           if (timed_out(deadline)) {
             __hip_atomic_store(errw, 1u, RLX_AGENT);
             s_tmo = 1;
-            break;
-          }
-          if ((npass % PICP_SWEEP_ERR_PASSES) == 0 && __hip_atomic_load(errw, RLX_AGENT) != 0u) {
-            s_tmo = 1;  // another block timed out: its partials may never come
             break;
           }
           PICP_POLL_PAUSE();
