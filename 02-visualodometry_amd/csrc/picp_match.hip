@@ -918,10 +918,12 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   }
   const int64_t blocks_rb2 = (int64_t)n_problems * ((max_nq + 2 * 32 * MM_WAVES - 1) / (2 * 32 * MM_WAVES));
   // (measured for the folded accept-only form only; the others need 130-224 VGPRs at RB = 2)
-  // ... or when an occupancy split of 8+ ranges already multiplies the grid (few problems against
-  // long reference sets: the 8e world match, 43.9k -> 44.8k frames/s; at the per-rank shape's 4
-  // ranges RB = 2 measured 2.4 % slower; profiles/r06/t3/ab.log)
-  int rb = (fold && (blocks_rb2 >= 4 * (int64_t)num_cu || ksplit >= 8)) ? 2 : 1;
+  // ... or when an occupancy split of 8+ ranges already multiplies the grid to >= 2 blocks per CU
+  // (few problems against long reference sets: the 8e world match's 4 problems x 15 ranges, +1.5-2 %;
+  // at the per-rank shape's 4 ranges RB = 2 measured 2.4 % slower, and one problem's 16 ranges at
+  // RB = 2 leave half the CUs idle: profiles/r06/t3/ab.log, profiles/r06/final/)
+  int rb = (fold && (blocks_rb2 >= 4 * (int64_t)num_cu ||
+                     (ksplit >= 8 && blocks_rb2 * ksplit >= 2 * (int64_t)num_cu))) ? 2 : 1;
   if (const char* e = getenv("PICP_MATCH_RB")) rb = (atoi(e) == 2) ? 2 : 1;
   const int qpb = MM_WAVES * 32 * rb;
   const int gx = (int)((max_nq + qpb - 1) / qpb);
