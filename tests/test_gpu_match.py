@@ -166,8 +166,9 @@ def test_match_batch_two_row_blocks(native, oracle, monkeypatch):
         _eq(got, oracle.match_points(d1, d2))
 
 
+@pytest.mark.parametrize("rb", ["default", "2"])
 @pytest.mark.parametrize("ksplit", ["1", "3", "5", "16"])
-def test_match_reference_range_split(native, oracle, monkeypatch, ksplit):
+def test_match_reference_range_split(native, oracle, monkeypatch, ksplit, rb):
     """The reference-range split (picp_match_ksplit: few problems against many references, e.g.
     the VO world match of a few long segments): each range's top-2 is merged in range order
     (picp_match_merge_kernel).  PICP_MATCH_KSPLIT forces the range count; ranges are >= 1,024 rows,
@@ -175,6 +176,8 @@ def test_match_reference_range_split(native, oracle, monkeypatch, ksplit):
     lower index must win and second = best), a triple duplicate across three ranges, near-ties
     across a boundary, and a ragged batch with empty sets."""
     monkeypatch.setenv("PICP_MATCH_KSPLIT", ksplit)
+    if rb != "default":  # two row blocks per wave with the split (the 8e world match's form since round 6)
+        monkeypatch.setenv("PICP_MATCH_RB", rb)
     rng = np.random.default_rng(77)
     d2 = rng.uniform(-1, 1, (5000, 10)).astype(np.float32)
     d2[1024] = d2[1023]                                   # boundary of ranges 0 | 1
