@@ -1325,69 +1325,6 @@ __device__ __forceinline__ void tri_null_jacobi(double A[4][4], double v[4]) {
   }
 }
 
-// The same null vector from M = A^T A (10 unique doubles instead of A's 16) by the two-sided
-// cyclic Jacobi eigen-iteration -- the oracle's own method (Jacobi on A^T A, in long double there):
-// rotate (p, q) while |m_pq| > 1e-12 sqrt(m_pp m_qq) (the one-sided form's orthogonality threshold,
-// as m_pq = a_p . a_q), at most 10 sweeps, then the column of V with the smallest diagonal.  About
-// 60 VGPRs live instead of ~100: the append's blocks then fit beside the matcher's (A/B,
-// -DPICP_TRI_SYM, with VOA_BLOCK 256).
-__device__ __forceinline__ void tri_null_jacobi_sym(const double A[4][4], double v[4]) {
-  double m[4][4];  // upper triangle used (compile-time indices: registers)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = i; j < 4; ++j) m[i][j] = A[0][i] * A[0][j] + A[1][i] * A[1][j] + A[2][i] * A[2][j] + A[3][i] * A[3][j];
-  double Vm[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) Vm[r][c] = (r == c) ? 1.0 : 0.0;
-  auto M = [&](int i, int j) -> double& { return (i <= j) ? m[i][j] : m[j][i]; };
-  for (int sweep = 0; sweep < 10; ++sweep) {
-    bool rotated = false;
-#pragma unroll
-    for (int pq = 0; pq < 6; ++pq) {
-      const int p = (pq < 3) ? 0 : ((pq < 5) ? 1 : 2);
-      const int q = (pq < 3) ? pq + 1 : ((pq < 5) ? pq - 1 : 3);
-      const double apq = M(p, q), app = M(p, p), aqq = M(q, q);
-      if (fabs(apq) > 1e-300 && apq * apq > 1e-24 * (app * aqq)) {
-        rotated = true;
-        const double theta = (aqq - app) * tri_rcp(2.0 * apq);
-        const double th2 = fma(theta, theta, 1.0);
-        const double t = ((theta >= 0.0) ? 1.0 : -1.0) * tri_rcp(fabs(theta) + th2 * tri_rsq(th2));
-        const double c = tri_rsq(fma(t, t, 1.0));
-        const double sn = c * t;
-        M(p, p) = app - t * apq;
-        M(q, q) = aqq + t * apq;
-        M(p, q) = 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (r != p && r != q) {
-            const double arp = M(r, p), arq = M(r, q);
-            M(r, p) = c * arp - sn * arq;
-            M(r, q) = sn * arp + c * arq;
-          }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const double vkp = Vm[k][p], vkq = Vm[k][q];
-          Vm[k][p] = c * vkp - sn * vkq;
-          Vm[k][q] = sn * vkp + c * vkq;
-        }
-      }
-    }
-    if (!rotated) break;
-  }
-  double best = m[0][0];
-  v[0] = Vm[0][0]; v[1] = Vm[1][0]; v[2] = Vm[2][0]; v[3] = Vm[3][0];
-#pragma unroll
-  for (int c = 1; c < 4; ++c) {
-    const bool take = m[c][c] < best;
-    best = take ? m[c][c] : best;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = take ? Vm[r][c] : v[r];
-  }
-}
-
 // Two-view linear (DLT) triangulation of one point, cv::triangulatePoints as called from
 // src/cam.cpp:115 then convertPointsFromHomogeneous :118.  P1, P2: 3x4 ROW-major float.
 // A (4x4) in double; X_h = the right singular vector of A's smallest singular value, by the
@@ -1414,9 +1351,7 @@ __device__ inline void triangulate_dlt(const float* P1, const float* P2, float2 
     A[3][k] = (double)b.y * (double)P2[8 + k] - (double)P2[4 + k];
   }
   double v[4];
-#if defined(PICP_TRI_SYM)
-  tri_null_jacobi_sym(A, v);
-#elif !defined(PICP_TRI_INVIT)
+#ifndef PICP_TRI_INVIT
   tri_null_jacobi(A, v);
 #else
   {

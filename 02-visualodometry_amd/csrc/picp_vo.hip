@@ -109,10 +109,7 @@ __global__ __launch_bounds__(VO_BLOCK) void vo_gather_kernel(const VoArgs a, int
   if (threadIdx.x == 0) a.probs[s] = PicpProblem{base, (int32_t)cnt, 0, 1, 0};
 }
 
-#ifndef VOA_MINB
-#define VOA_MINB 1
-#endif
-__global__ __launch_bounds__(VOA_BLOCK, VOA_MINB) void vo_append_kernel(const VoArgs a, int t) {
+__global__ __launch_bounds__(VOA_BLOCK) void vo_append_kernel(const VoArgs a, int t) {
   const int s = a.seg0 + (int)blockIdx.x;
   vo_append_body<VOA_BLOCK>(a, t, s, a.st_out + s, (t < 0) ? 0 : a.probs[s].n);
 }
