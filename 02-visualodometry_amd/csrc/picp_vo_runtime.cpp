@@ -241,8 +241,9 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   // 597-600k frames/s with two, round 2), and so did four and eight at the
   // latency-bound shapes, where a step waits for its chain's slowest segment (round 6: 8e
   // 32.5k / 18.4k vs 42.0k frames/s, the N = 8 per-rank shape 90.2k / 50.0k vs 156.9k;
-  // profiles/r06/t2/ab.log): the chains share 4 hardware queues
-  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(8, atoi(e)));
+  // profiles/r06/t2/ab.log), also with 16 hardware queues (8e 30.1k / 28.5k, t6) and replayed
+  // from a hipGraph (11.3k-25.8k, t7): the extra chains' world matches compete for the chip
+  if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
