@@ -15,6 +15,17 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
                                              float ratio_thr, int32_t* best_idx, float* best_dist,
                                              float* second_dist, int32_t* accepted, int form, int ksplit,
                                              float4* part, int64_t part_cap);
+extern "C" hipError_t picp_launch_match_mfma_parts(hipStream_t stream, int n_problems, int64_t max_nq,
+                                                   const float* q_desc, const float* r_desc, const _Float16* q_h,
+                                                   const float* q_n1, const _Float16* r_h, const float* r_n1,
+                                                   const float* r_n2, const struct MatchProblem* probs, int dim,
+                                                   float dist_thr, float ratio_thr, int form, int ksplit, int slot0,
+                                                   float4* part, int64_t part_cap);
+extern "C" hipError_t picp_launch_match_merge(hipStream_t stream, const struct MatchProblem* probs, int n_problems,
+                                              int64_t max_nq, int ksplit, int extra, const float4* part,
+                                              int64_t part_cap, float dist_thr, float ratio_thr,
+                                              int32_t* best_idx, float* best_dist, float* second_dist,
+                                              int32_t* accepted);
 // picp_match_ksplit reads PICP_MATCH_KSPLIT each call; picp_match_ksplit_forced takes the forced
 // count (0: none) from the caller, so a handle can read the variable once and size its scratch and
 // its launches from the same value

@@ -98,6 +98,9 @@ static_assert(sizeof(PicpProblem) % 8 == 0, "PicpProblem alignment");
 
 struct MatchProblem {
   int64_t q_off, nq, r_off, nr;
+  // the index of reference r_off in the caller's numbering (0: indices relative to r_off): a
+  // problem over a later part of a reference set reports indices in the whole set's numbering
+  int64_t idx0;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -159,6 +162,14 @@ struct VoArgs {     // by value; every pointer is device memory
   PicpState* st_in;
   const PicpState* st_out;
   MatchProblem* wprobs;      // next step's world-match problem of each segment
+  // the world match split by map age (split != 0; picp_vo_runtime.cpp): the append of step t
+  // writes the LATE part of step t + 1 (the points it added) and the EARLY part of step t + 2
+  // (the map as it leaves it), the latter double-buffered by step parity:
+  // eprobs[(step & 1) * seg_all + s]
+  MatchProblem* lprobs;
+  MatchProblem* eprobs;
+  int32_t split;
+  int32_t seg_all;           // segments of the handle (eprobs' parity stride)
   float* poses;              // 16 per slot, camera-in-world, column-major
   VoStep* steps;
   int2* pairs;               // append scratch: segment s at s * cap_c

@@ -244,6 +244,11 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #ifndef MM_RT
 #define MM_RT 256  // reference rows per LDS tile (128: -3.4 % on C5, 512: -7 %; profiles/r01/match_ab.log)
 #endif
+// tiles of references in flight ahead of the one computed (pass 2): 1 or 2
+#ifndef MM_PF
+#define MM_PF 1
+#endif
+static_assert(MM_PF == 1 || MM_PF == 2, "MM_PF: 1 or 2");
 #ifndef MM_BT
 #define MM_BT 4  // folded pass: column blocks whose B operands are read per LDS wait (RB = 1)
 #endif
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const MatchProblem* __restrict__ probs, int dim, float dist_thr, float ratio_thr,
     int32_t* __restrict__ best_idx, float* __restrict__ best_dist,
     float* __restrict__ second_dist, int32_t* __restrict__ accepted, int n_problems, int gx,
-    int xcd_map, int ksplit, float4* __restrict__ part, int64_t part_nq) {
+    int xcd_map, int ksplit, float4* __restrict__ part, int64_t part_nq, int slot0) {
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
@@ -427,14 +432,16 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   const int64_t nr_all = P.nr;
   // fetch tile t0 into registers (chunk tid + k*MM_BLOCK; norm tid + k*MM_BLOCK of the tile's
   // [n1 | n2] block), stash them into buffer b
-  mm_half8 stg[CPT];
-  float sn[NPN];
-  auto fetch = [&](int64_t t0) {
+  // the stage registers: tile t + 1 in flight while tile t is computed (MM_PF = 2: tiles t + 1 and
+  // t + 2, in two stages whose roles alternate between consecutive tiles)
+  mm_half8 stg[CPT], stg2[CPT];
+  float sn[NPN], sn2[NPN];
+  auto fetch_to = [&](int64_t t0, mm_half8 (&g)[CPT], float (&gn)[NPN]) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int ch = tid + k * MM_BLOCK;
       const int64_t row = min(t0 + ch / (DP / 8), nr_all - 1);
-      stg[k] = *reinterpret_cast<const mm_half8*>(r_h + (P.r_off + row) * DP + (ch % (DP / 8)) * 8);
+      g[k] = *reinterpret_cast<const mm_half8*>(r_h + (P.r_off + row) * DP + (ch % (DP / 8)) * 8);
       if constexpr (RAD == 2) {
         // a row past the end folds to S' = -65504 + tau/2 < 0 (never a candidate): components
         // zero, -n2s/2 hi = -65504, lo = 0, and its [1, 1] slots zero too -- so a partial tile
@@ -442,32 +449,35 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         if (t0 + ch / (DP / 8) >= nr_all) {
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            stg[k][e] = ((ch % (DP / 8)) * 8 + e == dim) ? (_Float16)-65504.0f : (_Float16)0.0f;
+            g[k][e] = ((ch % (DP / 8)) * 8 + e == dim) ? (_Float16)-65504.0f : (_Float16)0.0f;
         }
       }
     }
 #pragma unroll
     for (int k = 0; k < NPN; ++k) {
       const int idx = tid + k * MM_BLOCK, nt = idx % MM_RT;
-      sn[k] = ((idx < MM_RT) ? r_n1 : r_n2)[P.r_off + min(t0 + nt, nr_all - 1)];
+      gn[k] = ((idx < MM_RT) ? r_n1 : r_n2)[P.r_off + min(t0 + nt, nr_all - 1)];
     }
   };
+  auto fetch = [&](int64_t t0) { fetch_to(t0, stg, sn); };
   // RAD = 2: a tile is folded iff it is whole and every reference in it is inside the fold's
   // range (n1 <= 60000: finite, safe); each thread checks the n1 norms it fetched
   int my_nofold = 0;
-  auto fold_check = [&](int64_t t0) {
+  auto fold_check_of = [&](const float (&gn)[NPN]) {
     int bad = 0;  // rows past the end are neutralised by fetch (their clamped norms are safe)
 #pragma unroll
     for (int k = 0; k < NPN; ++k)
-      if (tid + k * MM_BLOCK < MM_RT) bad |= (sn[k] <= MM_FOLD_MAX) ? 0 : 1;
+      if (tid + k * MM_BLOCK < MM_RT) bad |= (gn[k] <= MM_FOLD_MAX) ? 0 : 1;
     return bad;
   };
-  auto stash = [&](int b) {
+  auto fold_check = [&](int64_t) { return fold_check_of(sn); };
+  auto stash_from = [&](int b, const mm_half8 (&g)[CPT], const float (&gn)[NPN]) {
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) s_t[b][tid + k * MM_BLOCK] = stg[k];
+    for (int k = 0; k < CPT; ++k) s_t[b][tid + k * MM_BLOCK] = g[k];
 #pragma unroll
-    for (int k = 0; k < NPN; ++k) (&s_n[b][0][0])[tid + k * MM_BLOCK] = sn[k];
+    for (int k = 0; k < NPN; ++k) (&s_n[b][0][0])[tid + k * MM_BLOCK] = gn[k];
   };
+  auto stash = [&](int b) { stash_from(b, stg, sn); };
   auto load_b = [&](int b, int col, mm_half8* bb) {
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bb[c] = s_t[b][col * (DP / 8) + 2 * c + hf];
@@ -536,8 +546,10 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) b1[rb][i] = s1[rb][i] = INFINITY;
   float rmax = 0.0f;
-  fetch(0);
-  stash(0);
+  if (nr_all > 0) {
+    fetch(0);
+    stash(0);
+  }
   buf = 0;
   for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
     __syncthreads();
@@ -614,16 +626,16 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       ++c_n;
     }
   };
-  fetch(0);
-  if constexpr (RAD == 2) my_nofold = fold_check(0);
-  stash(0);
-  buf = 0;
-  for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
+  // One tile: fold vote (RAD = 2) and barrier, the fetch MM_PF tiles ahead into stage fs, the
+  // compute on LDS buffer b, then the next tile's stage rs (already in flight) stashed into b ^ 1.
+  auto tile_step = [&](int64_t t0, int b, mm_half8 (&fs)[CPT], float (&fn)[NPN], mm_half8 (&rs)[CPT],
+                       float (&rn)[NPN]) {
+    const int buf = b;
     bool fold = false;
     if constexpr (RAD == 2) fold = __syncthreads_or(my_nofold) == 0;
     else __syncthreads();
     const bool more = t0 + MM_RT < nr_all;
-    if (more) fetch(t0 + MM_RT);
+    if (t0 + MM_PF * MM_RT < nr_all) fetch_to(t0 + MM_PF * MM_RT, fs, fn);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
       // the B operands of BT column blocks first (one LDS wait per group, not per block);
@@ -644,6 +656,27 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         // VGPRs, 4 -> 3 waves) and 1,024 x 2,000 x 2,000 took 353 instead of 316 us, C5 619k
         // instead of 632-635k frames/s (profiles/r03/mab/).
         constexpr int NQB = BT * RB;
+#ifdef MM_PAIRVOTE
+        // A/B: both row blocks of a column block (one B operand) issued back to back, one max tree
+        // over the two accumulators and one wave vote for the pair
+        if constexpr (RB == 2) {
+#pragma unroll
+          for (int kb = 0; kb < BT; ++kb) {
+            const mm_f16v a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[kb], (mm_f16v){}, 0, 0, 0);
+            const mm_f16v a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[1], bt[kb], (mm_f16v){}, 0, 0, 0);
+            int mx = __float_as_int(a0[0]);
+#pragma unroll
+            for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(a0[i]));
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = max(mx, __float_as_int(a1[i]));
+            if (__any(mx >= 0)) {
+              push_mask(mm_pack16(mm_mask16_rows(a0)), t0, sg + kb, 0);
+              push_mask(mm_pack16(mm_mask16_rows(a1)), t0, sg + kb, 1);
+            }
+          }
+          continue;
+        }
+#endif
         mm_f16v accs[2];
 #ifdef MM_PIPE
         accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[0], (mm_f16v){}, 0, 0, 0);
@@ -665,9 +698,18 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
             // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
             // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
             // v_max3 here read the accumulator before the MFMA had written it).
+#ifdef MM_TREE
+            // A/B: a balanced max3 tree (dependent depth 3 instead of 8)
+            auto ai = [&](int i) { return __float_as_int(acc[i]); };
+            const int m0 = max(max(ai(0), ai(1)), ai(2)), m1 = max(max(ai(3), ai(4)), ai(5));
+            const int m2 = max(max(ai(6), ai(7)), ai(8)), m3 = max(max(ai(9), ai(10)), ai(11));
+            const int m4 = max(max(ai(12), ai(13)), ai(14));
+            const int mx = max(max(max(m0, m1), m2), max(max(m3, m4), ai(15)));
+#else
             int mx = __float_as_int(acc[0]);
 #pragma unroll
             for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
+#endif
 #ifdef MM_DIAG_NOVOTE  // diagnostic timing build only: MFMA + max tree, no vote, no candidates
             if (mx == 0x7fffffff) c_n = 0;
             if (false) {
@@ -687,10 +729,10 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
       }  // column-block group
       if (more) {
-        my_nofold = fold_check(t0 + MM_RT);  // after the compute: the fetch has landed by now
-        stash(buf ^ 1);
+        my_nofold = fold_check_of(rn);  // after the compute: the fetch has landed by now
+        stash_from(buf ^ 1, rs, rn);
       }
-      continue;
+      return;
     }
 #pragma unroll 1
     for (int sub = 0; sub < MM_RT / 32; ++sub) {
@@ -713,8 +755,25 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       }
     }
     if (more) {
-      if constexpr (RAD == 2) my_nofold = fold_check(t0 + MM_RT);
-      stash(buf ^ 1);
+      if constexpr (RAD == 2) my_nofold = fold_check_of(rn);
+      stash_from(buf ^ 1, rs, rn);
+    }
+  };
+  if (nr_all > 0) {  // an empty reference set (a late part with no new points): no tile
+    fetch(0);
+    if constexpr (RAD == 2) my_nofold = fold_check(0);
+    stash(0);
+  }
+  if constexpr (MM_PF == 1) {
+    for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += MM_RT, b ^= 1) tile_step(t0, (int)b, stg, sn, stg, sn);
+  } else {
+    // tile 1 into stg before the loop; the stages alternate: tile t's step fills one while the
+    // other (tile t + 1, fetched a step earlier) is stashed
+    if (MM_RT < nr_all) fetch(MM_RT);
+    for (int64_t t0 = 0; t0 < nr_all; t0 += 2 * MM_RT) {
+      tile_step(t0, 0, stg2, sn2, stg, sn);
+      if (t0 + MM_RT >= nr_all) break;
+      tile_step(t0 + MM_RT, 1, stg, sn, stg2, sn2);
     }
   }
   // expand the lane lists into the per-query lists (the same LDS words): every entry of the wave
@@ -813,11 +872,13 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
       }
     }
-    if (ksplit > 1)  // this range's top-2 (global index), merged in range order by picp_match_merge_kernel
-      part[((int64_t)ks * n_problems + pid) * part_nq + qi] =
-          make_float4(__int_as_float(bi >= 0 ? (int32_t)(bi + r_lo) : -1), best, second, 0.0f);
+    // indices in the caller's numbering: the range's offset and the problem's idx0
+    const int32_t gi = bi >= 0 ? (int32_t)(bi + r_lo + P.idx0) : -1;
+    if (ksplit > 1 || slot0 >= 0)  // this range's top-2, merged in range order by picp_match_merge_kernel
+      part[((int64_t)(max(slot0, 0) + ks) * n_problems + pid) * part_nq + qi] =
+          make_float4(__int_as_float(gi), best, second, 0.0f);
     else
-      match_store(P, P.q_off + qi, bi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
+      match_store(P, P.q_off + qi, gi, best, second, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
                   accepted);  // :100-103
   }
 }
@@ -832,12 +893,15 @@ __global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, 
                                                    int ksplit, const float4* __restrict__ part, int64_t part_nq,
                                                    float dist_thr, float ratio_thr, int32_t* __restrict__ best_idx,
                                                    float* __restrict__ best_dist, float* __restrict__ second_dist,
-                                                   int32_t* __restrict__ accepted) {
+                                                   int32_t* __restrict__ accepted, int extra) {
   const int pid = blockIdx.y;
   const MatchProblem P = probs[pid];
   const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (qi >= P.nq) return;
-  const int ns = mm_nsplit(P.nr, ksplit);
+  // the problem's ranges, then (extra >= 0) slot `extra`: a range of later references (higher
+  // indices) written by another launch
+  const int nsr = mm_nsplit(P.nr, ksplit);
+  const int ns = nsr + (extra >= 0 ? 1 : 0);
   float best = FLT_MAX, second = FLT_MAX;  // src/my_utilities.h:78-79
   int32_t bi = -1;
   // the ranges in chunks of MM_MERGE_CHUNK (4 or 16: the launch's ksplit rounded up), every load of a
@@ -847,7 +911,10 @@ __global__ void picp_match_merge_kernel(const MatchProblem* __restrict__ probs, 
     float4 rr[MM_MERGE_CHUNK];
 #pragma unroll
     for (int u = 0; u < MM_MERGE_CHUNK; ++u)  // unconditional (clamped) loads: no branch between them
-      rr[u] = part[((int64_t)min(k0 + u, ns - 1) * n_problems + pid) * part_nq + qi];
+    {
+      const int k = min(k0 + u, ns - 1);
+      rr[u] = part[((int64_t)(k < nsr ? k : extra) * n_problems + pid) * part_nq + qi];
+    }
 #pragma unroll
     for (int u = 0; u < MM_MERGE_CHUNK; ++u) {
       const float4 r = rr[u];
@@ -884,20 +951,37 @@ extern "C" hipError_t picp_launch_match_prep(hipStream_t stream, const float* de
 // PICP_MATCH_FORM_*): bit 0 = the accept-only radius form (only accepted[] and the best index of
 // accepted queries are defined), bit 1 = the exact scan (the same results as the full form; for
 // A/B checks and the tests).
-extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
-                                             const float* q_desc, const float* r_desc,
-                                             const _Float16* q_h, const float* q_n1,
-                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
-                                             const MatchProblem* probs, int dim, float dist_thr,
-                                             float ratio_thr, int32_t* best_idx, float* best_dist,
-                                             float* second_dist, int32_t* accepted, int form, int ksplit,
-                                             float4* part, int64_t part_cap) {
+static hipError_t mm_merge(hipStream_t stream, const MatchProblem* probs, int n_problems, int64_t max_nq, int ksplit,
+                           int extra, const float4* part, float dist_thr, float ratio_thr, int32_t* best_idx,
+                           float* best_dist, float* second_dist, int32_t* accepted) {
+  const dim3 mg((unsigned)((max_nq + 255) / 256), (unsigned)n_problems);
+  if (ksplit + (extra >= 0 ? 1 : 0) <= 4)
+    hipLaunchKernelGGL(picp_match_merge_kernel<4>, mg, dim3(256), 0, stream, probs, n_problems, ksplit, part, max_nq,
+                       dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, extra);
+  else
+    hipLaunchKernelGGL(picp_match_merge_kernel<16>, mg, dim3(256), 0, stream, probs, n_problems, ksplit, part, max_nq,
+                       dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, extra);
+  return hipGetLastError();
+}
+
+// slot0 < 0: the whole match (a split launch's ranges merged by a second launch); slot0 >= 0: the
+// ranges' partial top-2s only, into scratch slots slot0 .. slot0 + ksplit - 1 (picp_launch_match_merge
+// folds them with other launches' ranges)
+static hipError_t mm_launch(hipStream_t stream, int n_problems, int64_t max_nq, const float* q_desc,
+                            const float* r_desc, const _Float16* q_h, const float* q_n1, const _Float16* r_h,
+                            const float* r_n1, const float* r_n2, const MatchProblem* probs, int dim,
+                            float dist_thr, float ratio_thr, int32_t* best_idx, float* best_dist,
+                            float* second_dist, int32_t* accepted, int form, int ksplit, int slot0, float4* part,
+                            int64_t part_cap) {
   if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
   // part_cap: the scratch's capacity in float4; a split launch writes ksplit x n_problems x max_nq
-  if (ksplit < 1 || ksplit > MM_KSPLIT_LIMIT) return hipErrorInvalidValue;
-  if (ksplit > 1 && (!part || (int64_t)ksplit * n_problems * max_nq > part_cap)) return hipErrorInvalidValue;
+  if (ksplit < 1 || ksplit > MM_KSPLIT_LIMIT || slot0 > MM_KSPLIT_LIMIT) return hipErrorInvalidValue;
+  const bool parts = ksplit > 1 || slot0 >= 0;
+  if (parts && (!part || (int64_t)(std::max(slot0, 0) + ksplit) * n_problems * max_nq > part_cap))
+    return hipErrorInvalidValue;
   const bool accept_only = (form & 1) != 0;
   if (dim < 1 || dim > PICP_MATCH_MAXD || n_problems > 65535) return hipErrorInvalidValue;
+  if (slot0 >= 0 && (form & 2)) return hipErrorInvalidValue;  // the exact scan writes no partials
   // the radius argument needs 0 < dist_thr < inf and 0 < ratio_thr <= 1 (else: the full form)
   const bool rad = accept_only && dist_thr > 0.0f && dist_thr < 1e30f && ratio_thr > 0.0f && ratio_thr <= 1.0f;
   // the folded form needs the extension slots (dim <= 12) and tau/2 inside fp16 range
@@ -938,7 +1022,7 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
 #define PICP_LAUNCH_MM3(KC, RD, R)                                                                          \
   hipLaunchKernelGGL((picp_match_mfma_kernel<KC, RD, R>), g, dim3(MM_BLOCK), 0, stream, q_desc, r_desc, q_h,  \
                      q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr, ratio_thr, best_idx, best_dist, second_dist, \
-                     accepted, n_problems, gx, xcd_map, ksplit, part, part_nq)
+                     accepted, n_problems, gx, xcd_map, ksplit, part, part_nq, slot0)
 #define PICP_LAUNCH_MM(KC, RD)                   \
   {                                              \
     if (rb == 2) PICP_LAUNCH_MM3(KC, RD, 2);     \
@@ -954,20 +1038,54 @@ extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems,
   }
 #undef PICP_LAUNCH_MM3
 #undef PICP_LAUNCH_MM
-  if (ksplit > 1) {
+  if (ksplit > 1 && slot0 < 0) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const dim3 mg((unsigned)((max_nq + 255) / 256), (unsigned)n_problems);
-    if (ksplit <= 4)
-      hipLaunchKernelGGL(picp_match_merge_kernel<4>, mg, dim3(256), 0, stream, probs, n_problems, ksplit,
-                         (const float4*)part, part_nq, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                         accepted);
-    else
-      hipLaunchKernelGGL(picp_match_merge_kernel<16>, mg, dim3(256), 0, stream, probs, n_problems, ksplit,
-                         (const float4*)part, part_nq, dist_thr, ratio_thr, best_idx, best_dist, second_dist,
-                         accepted);
+    return mm_merge(stream, probs, n_problems, max_nq, ksplit, -1, part, dist_thr, ratio_thr, best_idx, best_dist,
+                    second_dist, accepted);
   }
   return hipGetLastError();
+}
+
+extern "C" hipError_t picp_launch_match_mfma(hipStream_t stream, int n_problems, int64_t max_nq,
+                                             const float* q_desc, const float* r_desc,
+                                             const _Float16* q_h, const float* q_n1,
+                                             const _Float16* r_h, const float* r_n1, const float* r_n2,
+                                             const MatchProblem* probs, int dim, float dist_thr,
+                                             float ratio_thr, int32_t* best_idx, float* best_dist,
+                                             float* second_dist, int32_t* accepted, int form, int ksplit,
+                                             float4* part, int64_t part_cap) {
+  return mm_launch(stream, n_problems, max_nq, q_desc, r_desc, q_h, q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr,
+                   ratio_thr, best_idx, best_dist, second_dist, accepted, form, ksplit, -1, part, part_cap);
+}
+
+// The partial top-2s of ksplit ranges of each problem's references into scratch slots slot0 ..
+// slot0 + ksplit - 1 (no outputs written; the pre-filtered forms only)
+extern "C" hipError_t picp_launch_match_mfma_parts(hipStream_t stream, int n_problems, int64_t max_nq,
+                                                   const float* q_desc, const float* r_desc, const _Float16* q_h,
+                                                   const float* q_n1, const _Float16* r_h, const float* r_n1,
+                                                   const float* r_n2, const MatchProblem* probs, int dim,
+                                                   float dist_thr, float ratio_thr, int form, int ksplit, int slot0,
+                                                   float4* part, int64_t part_cap) {
+  if (slot0 < 0) return hipErrorInvalidValue;
+  return mm_launch(stream, n_problems, max_nq, q_desc, r_desc, q_h, q_n1, r_h, r_n1, r_n2, probs, dim, dist_thr,
+                   ratio_thr, nullptr, nullptr, nullptr, nullptr, form, ksplit, slot0, part, part_cap);
+}
+
+// The outputs of problems probs from scratch: the mm_nsplit(nr, ksplit) ranges of each problem in
+// slots 0.., then (extra >= 0) slot extra, whose references all come after the problem's (higher
+// indices) -- the reference's in-order scan over the problem's references continued over them
+extern "C" hipError_t picp_launch_match_merge(hipStream_t stream, const MatchProblem* probs, int n_problems,
+                                              int64_t max_nq, int ksplit, int extra, const float4* part,
+                                              int64_t part_cap, float dist_thr, float ratio_thr,
+                                              int32_t* best_idx, float* best_dist, float* second_dist,
+                                              int32_t* accepted) {
+  if (n_problems <= 0 || max_nq <= 0) return hipSuccess;
+  if (n_problems > 65535 || ksplit < 1 || ksplit > MM_KSPLIT_LIMIT || extra > MM_KSPLIT_LIMIT || !part)
+    return hipErrorInvalidValue;
+  if ((int64_t)std::max(ksplit, extra + 1) * n_problems * max_nq > part_cap) return hipErrorInvalidValue;
+  return mm_merge(stream, probs, n_problems, max_nq, ksplit, extra, part, dist_thr, ratio_thr, best_idx, best_dist,
+                  second_dist, accepted);
 }
 
 // The reference-range split a launch of this shape takes (1: none): enough (problem, query block,

@@ -219,6 +219,20 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
       wp.nq = a.frame_off[f + 1] - wp.q_off;
     }
     a.wprobs[s] = wp;
+    if (a.split) {
+      // the late part of step tn: frame f0+tn+1 against the points this append added (indices in
+      // the whole map's numbering) ...
+      a.lprobs[s] = MatchProblem{wp.q_off, wp.nq, G.map_off + s_base, cnt, s_base};
+      // ... and the early part of step tn + 1: frame f0+tn+2 against the map as it is now
+      const int te = tn + 1;
+      MatchProblem ep{0, 0, G.map_off, mn, 0};
+      if (te < G.steps) {
+        const int64_t f = G.f0 + te + 1;
+        ep.q_off = a.frame_off[f];
+        ep.nq = a.frame_off[f + 1] - ep.q_off;
+      }
+      a.eprobs[(int64_t)(te & 1) * a.seg_all + s] = ep;
+    }
     // PICP initial state: world-in-camera = previous_pose.inverse() (:78)
     float Twc[16];
     vo_iso_inverse(sTn, Twc);

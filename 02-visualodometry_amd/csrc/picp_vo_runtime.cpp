@@ -115,6 +115,21 @@ struct picp_vo {
   std::vector<float4*> part_w;    // [chains]
   std::vector<int64_t> cap_w;     // [chains]: part_w's capacity, float4
   std::vector<std::pair<size_t, int>> ks_p;  // frame->next launch starting at problem .first: split .second
+  // The world match split by map age (PICP_VO_SPLIT; default: the chains whose world match is
+  // range-split, i.e. few segments against long maps).  Step t matches frame f0+t+1 against the map
+  // after step t-1's append.  The map is append-only, so that is the EARLY part -- the map as step
+  // t-2's append left it, which needs nothing from step t-1 and runs on the chain's early stream
+  // beside step t-1 -- and the LATE part, the points step t-1's append added.  Only the late part
+  // and the merge stay on the chain: the merge kernel folds the early ranges and then the late one,
+  // the reference's in-order scan over the whole map (the late indices are the map's: idx0).
+  int split_env = -1;                 // PICP_VO_SPLIT: -1 auto, 0 off, 1 every chain
+  std::vector<char> split_c;          // [chains]
+  std::vector<float4*> part_e;        // [chains][2]: early ranges + the late slot, by step parity
+  std::vector<int64_t> cap_e;         // [chains]
+  std::vector<hipStream_t> estream;   // [chains]
+  std::vector<hipEvent_t> ev_app;     // [chains]: the chain's latest append
+  std::vector<hipEvent_t> ev_early;   // [chains][2]: the early part of step t done (by parity)
+  hipEvent_t ev_boot = nullptr;       // the bootstrap append (step 1's early parts may start)
   float4* part_p = nullptr;
   int64_t cap_p = 0;
   // the step's gather runs inside the PICP block kernel (picp_launch_vo_block) when every frame's
@@ -185,6 +200,13 @@ extern "C" int picp_vo_destroy(picp_vo_t* h) {
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->ev_ph)
     if (e) hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_app)
+    if (e) hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_early)
+    if (e) hipEventDestroy(e);
+  if (h->ev_boot) hipEventDestroy(h->ev_boot);
+  for (hipStream_t c : h->estream)
+    if (c) hipStreamDestroy(c);
   for (hipStream_t c : h->cstream)
     if (c) hipStreamDestroy(c);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -246,6 +268,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
+  if (const char* e = getenv("PICP_VO_SPLIT")) h->split_env = atoi(e) != 0 ? 1 : 0;
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \
@@ -282,6 +305,19 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
       if (c > 0) HIP_TRY(hipStreamCreateWithPriority(&h->cstream[c], hipStreamNonBlocking, hi));
       HIP_TRY(hipEventCreateWithFlags(&h->ev_cj[c], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&h->ev_ph[c], hipEventDisableTiming));
+    }
+    // the early world-match parts: throughput work beside the chains, at the side stream's priority
+    if (h->split_env != 0) {
+      h->estream.assign((size_t)h->chains, nullptr);
+      h->ev_app.assign((size_t)h->chains, nullptr);
+      h->ev_early.assign((size_t)2 * h->chains, nullptr);
+      for (int c = 0; c < h->chains; ++c) {
+        HIP_TRY(hipStreamCreateWithPriority(&h->estream[c], hipStreamNonBlocking, lo));
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_app[c], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c + 1], hipEventDisableTiming));
+      }
+      HIP_TRY(hipEventCreateWithFlags(&h->ev_boot, hipEventDisableTiming));
     }
     return PICP_OK;
   }());
@@ -418,6 +454,8 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_stin = part((size_t)n_seg * sizeof(PicpState));
   const Part p_stout = part((size_t)n_seg * sizeof(PicpState));
   const Part p_wprobs = part((size_t)n_seg * sizeof(MatchProblem));
+  const Part p_lprobs = part((size_t)n_seg * sizeof(MatchProblem));
+  const Part p_eprobs = part((size_t)2 * n_seg * sizeof(MatchProblem));
   const Part p_pprobs = part(std::max<size_t>(pprobs.size(), 1) * sizeof(MatchProblem));
   const Part p_poses = part((size_t)n_slots * 16 * sizeof(float));
   const Part p_steps = part((size_t)n_slots * sizeof(VoStep));
@@ -435,6 +473,17 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     ks_w[c] = picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only, ks_force);
     cap_w[c] = picp_match_split_scratch(ks_w[c], nsc, h->max_obs);
     p_partw.push_back(part((size_t)cap_w[c] * sizeof(float4)));
+  }
+  // the split by map age: a chain's early part takes the whole world match's range split, plus one
+  // slot for the late part (2 buffers: step t's merge and step t+2's early part overlap)
+  std::vector<char> split_c((size_t)chains_eff, 0);
+  std::vector<int64_t> cap_e((size_t)chains_eff, 0);
+  std::vector<Part> p_parte;
+  for (int c = 0; c < chains_eff; ++c) {
+    const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
+    split_c[c] = !h->estream.empty() && (h->split_env == 1 || (h->split_env < 0 && ks_w[c] > 1));
+    if (split_c[c]) cap_e[c] = (int64_t)(ks_w[c] + 1) * nsc * std::max<int64_t>(h->max_obs, 1);
+    p_parte.push_back(part((size_t)2 * cap_e[c] * sizeof(float4)));
   }
   // the frame->next launches, as vo_frame_match issues them: the whole table up front (overlap off)
   // or chunk by chunk, each in launches of at most VO_MAX_GRID_Y problems
@@ -472,6 +521,14 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   h->part_w.assign((size_t)chains_eff, nullptr);
   for (int c = 0; c < chains_eff; ++c)
     if (p_partw[c].bytes) h->part_w[c] = (float4*)(m + p_partw[c].off);
+  h->split_c = split_c;
+  h->cap_e = cap_e;
+  h->part_e.assign((size_t)2 * chains_eff, nullptr);
+  for (int c = 0; c < chains_eff; ++c)
+    if (split_c[c]) {
+      h->part_e[2 * c] = (float4*)(m + p_parte[c].off);
+      h->part_e[2 * c + 1] = h->part_e[2 * c] + cap_e[c];
+    }
   h->part_p = part_p_bytes ? (float4*)(m + p_partp.off) : nullptr;
   h->segs = segs;
   h->pprobs = pprobs;
@@ -532,6 +589,12 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   V.st_in = (PicpState*)(m + p_stin.off);
   V.st_out = (const PicpState*)(m + p_stout.off);
   V.wprobs = (MatchProblem*)(m + p_wprobs.off);
+  V.lprobs = (MatchProblem*)(m + p_lprobs.off);
+  V.eprobs = (MatchProblem*)(m + p_eprobs.off);
+  V.seg_all = n_seg;
+  // the append writes the split tables when any chain splits (one launch covers one chain)
+  V.split = 0;
+  for (int c = 0; c < chains_eff; ++c) V.split |= split_c[c] ? 1 : 0;
   V.poses = (float*)(m + p_poses.off);
   V.steps = (VoStep*)(m + p_steps.off);
   V.pairs = (int2*)(m + p_pairs.off);
@@ -639,6 +702,23 @@ static hipError_t vo_enqueue(picp_vo* h) {
   }
   if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const int C = std::min(h->chains_eff, h->n_seg);
+  bool any_split = false;
+  for (int c = 0; c < C; ++c) any_split = any_split || h->split_c[c];
+  // step u's early world-match part of chain c (the map as step u-2's append left it) on the
+  // chain's early stream; its ranges go to scratch slots 0.. of buffer u & 1
+  auto early_part = [&](int c, const VoArgs& V, int u) {
+    hipStream_t es = h->estream[c];
+    const int p = u & 1;
+    hipError_t r = hipSuccess;
+    if (!(skip & 8))
+      r = picp_launch_match_mfma_parts(es, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
+                                       V.map_h, V.map_n1, V.map_n2, V.eprobs + (size_t)p * h->n_seg + V.seg0,
+                                       h->dim, VO_MATCH_DIST, VO_MATCH_RATIO, h->accept_only, h->ks_w[c], 0,
+                                       h->part_e[2 * c + p], h->cap_e[c]);
+    if (r == hipSuccess) r = hipEventRecord(h->ev_early[2 * c + p], es);
+    return r;
+  };
+  if (e == hipSuccess && any_split) e = hipEventRecord(h->ev_boot, h->stream);
   // one world-match launch over chain c's segments [s0, s0 + n): tables probs (+ s0)
   auto world_match = [&](hipStream_t st, const VoArgs& V, const MatchProblem* probs, int c) {
     return picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
@@ -668,6 +748,12 @@ static hipError_t vo_enqueue(picp_vo* h) {
     for (int s = s0; s < s1; ++s) csteps[c] = std::max(csteps[c], (int)h->segs[s].steps);
     max_steps = std::max(max_steps, csteps[c]);
   }
+  // step 1's early parts: the map the bootstrap left
+  for (int c = 0; c < C && e == hipSuccess; ++c)
+    if (h->split_c[c] && csteps[c] > 1) {
+      e = hipStreamWaitEvent(h->estream[c], h->ev_boot, 0);
+      if (e == hipSuccess) e = early_part(c, cv[c], 1);
+    }
   for (int t = 0; t < max_steps && e == hipSuccess; ++t) {
     for (int c = 0; c < C && e == hipSuccess; ++c) {
       if (t >= csteps[c]) continue;
@@ -677,7 +763,23 @@ static hipError_t vo_enqueue(picp_vo* h) {
       (void)s1;
       // chain c starts after chain c-1's first world match (enqueued just before, at t = 0)
       if (t == 0 && c > 0) e = hipStreamWaitEvent(st, (h->phase ? h->ev_ph[c - 1] : h->ev_cj[0]), 0);
-      if (e == hipSuccess && !(skip & 8)) e = world_match(st, V, h->wprobs_d, c);
+      const bool sp = h->split_c[c] && t >= 1;
+      if (sp) {
+        // the late part into the slot after the early ranges, then the merge of both
+        const int p = t & 1;
+        e = hipStreamWaitEvent(st, h->ev_early[2 * c + p], 0);
+        if (e == hipSuccess && !(skip & 8))
+          e = picp_launch_match_mfma_parts(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
+                                           V.map_h, V.map_n1, V.map_n2, V.lprobs + s0, h->dim, VO_MATCH_DIST,
+                                           VO_MATCH_RATIO, h->accept_only, 1, h->ks_w[c], h->part_e[2 * c + p],
+                                           h->cap_e[c]);
+        if (e == hipSuccess && !(skip & 8))
+          e = picp_launch_match_merge(st, V.eprobs + (size_t)p * h->n_seg + s0, V.n_seg, h->max_obs, h->ks_w[c],
+                                      h->ks_w[c], h->part_e[2 * c + p], h->cap_e[c], VO_MATCH_DIST, VO_MATCH_RATIO,
+                                      h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc);
+      } else if (e == hipSuccess && !(skip & 8)) {
+        e = world_match(st, V, h->wprobs_d, c);
+      }
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
       if (fused) {
         if (e == hipSuccess && !(skip & 4)) e = picp_launch_vo_block(st, &V, t, h->npt, &h->pargs, h->max_obs);
@@ -693,6 +795,11 @@ static hipError_t vo_enqueue(picp_vo* h) {
 #endif
       if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
       if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
+      if (h->split_c[c] && t + 2 < csteps[c] && e == hipSuccess) {  // step t+2's early part
+        e = hipEventRecord(h->ev_app[c], st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->estream[c], h->ev_app[c], 0);
+        if (e == hipSuccess) e = early_part(c, V, t + 2);
+      }
     }
   }
   for (int c = 1; c < C && e == hipSuccess; ++c) e = hipEventRecord(h->ev_cj[c], cst[c]);

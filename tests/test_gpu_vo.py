@@ -261,6 +261,49 @@ def test_vo_step_schedules_bit_identical(native, monkeypatch):
             _assert_same_bits(ref, o, str(env))
 
 
+def _set_env(monkeypatch, env):
+    for k, v in env.items():
+        if v is None:
+            monkeypatch.delenv(k, raising=False)
+        else:
+            monkeypatch.setenv(k, v)
+
+
+def test_vo_split_world_match_bit_identical(native, monkeypatch):
+    """The world match split by map age (PICP_VO_SPLIT; on by default where a chain's world match
+    is range-split: few segments against long maps) -- the early part against the map two appends
+    old on its own stream, the late part against the last append's points, merged on the chain --
+    gives the unsplit schedule's poses, step records and maps bit for bit, in the serial order and
+    the concurrent schedule, run after run."""
+    from picp_amd.vo_synth import VOSequence, segments
+    n = 601
+    s = VOSequence(n, obs_per_frame=2000, seed=3)
+    F = s.frames(0, n)
+    first, steps = segments(n, 200)
+    rel = [np.linalg.inv(F["T_cw"][f].astype(np.float64)) for f in first]
+    boot = np.stack([[np.eye(4), rel[k] @ F["T_cw"][f + 1]] for k, f in enumerate(first)]).astype(np.float32)
+    ref = None
+    for env in ({"PICP_VO_SPLIT": "0", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
+                {"PICP_VO_SPLIT": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
+                {"PICP_VO_SPLIT": "0", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None},
+                {"PICP_VO_SPLIT": "1", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None},
+                {"PICP_VO_SPLIT": None, "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None}):
+        _set_env(monkeypatch, env)
+        outs = _vo_outputs(native, F, s.K, first, steps, boot)
+        if ref is None:
+            ref = outs[0]
+            assert min(int(r["n_corr"][1:].min()) for r in ref[1]) > 0
+        for o in outs:
+            _assert_same_bits(ref, o, str(env))
+
+
+def test_vo_split_world_match_vs_oracle(native, oracle, monkeypatch):
+    """The split world match forced on at test size: every step against the oracle (teacher
+    forcing), counts exact, as test_vo_synthetic_segments checks the default schedule."""
+    monkeypatch.setenv("PICP_VO_SPLIT", "1")
+    test_vo_synthetic_segments(native, oracle, 25, 600, 8, 0.0)
+
+
 @pytest.mark.parametrize("obs", [600, 2000, 2300])
 def test_vo_fused_gather_bit_identical(native, monkeypatch, obs):
     """The step's gather inside the PICP block kernel (default; the items reach registers and the
