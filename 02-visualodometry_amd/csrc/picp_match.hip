@@ -249,6 +249,9 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #define MM_PF 1
 #endif
 static_assert(MM_PF == 1 || MM_PF == 2, "MM_PF: 1 or 2");
+#ifndef MM_PIPE_RB2
+#define MM_PIPE_RB2 1  // 0: the RB = 2 folded loop unpipelined (A/B)
+#endif
 #ifndef MM_BT
 #define MM_BT 4  // folded pass: column blocks whose B operands are read per LDS wait (RB = 1)
 #endif
@@ -353,6 +356,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   constexpr int QPW = 32 * RB;                      // queries per wave
   constexpr int QPB = MM_WAVES * QPW;               // queries per block
   constexpr int BT = (RB == 2) ? MM_BT2 : MM_BT;
+  constexpr bool PIPE = MM_PIPE_RB2 && RB == 2;  // the folded loop software-pipelined (below)
   constexpr int DP = 16 * KCH;                      // halves per prepped row
   constexpr int CH = MM_RT * DP / 8;                // 16-B chunks per tile
   constexpr int CPT = CH / MM_BLOCK;                // 16-B chunks per thread per tile
@@ -649,12 +653,13 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
           load_b(buf, (sg + kb) * 32 + r, b1);
           bt[kb] = b1[0];
         }
-        // The group's BT x RB MFMA blocks are issued and consumed one at a time (an s_nop 11 after
-        // every MFMA); other waves of the SIMD fill the wait.  -DMM_PIPE (A/B): software-pipelined,
+        // RB = 1: the group's MFMA blocks are issued and consumed one at a time (an s_nop 11 after
+        // every MFMA); other waves of the SIMD fill the wait.  RB = 2 (PIPE): software-pipelined,
         // block q+1's MFMA issued into a second accumulator before block q's result is tested.
-        // Measured slower: the second accumulator costs a wave per SIMD (RB = 2: 108 -> 131
-        // VGPRs, 4 -> 3 waves) and 1,024 x 2,000 x 2,000 took 353 instead of 316 us, C5 619k
-        // instead of 632-635k frames/s (profiles/r03/mab/).
+        // Round 3 measured that slower (a wave per SIMD lost: 108 -> 131 VGPRs, profiles/r03/mab/);
+        // with the balanced max tree below it fits 120 VGPRs (four waves) and the default C5 shape
+        // ran 780k -> 799k frames/s (320 -> 313 us per chain step), the 8e partition +0.5 %; at RB = 1
+        // it cost the per-rank shape 1.5 % (profiles/r06/t12/ab.log).
         constexpr int NQB = BT * RB;
 #ifdef MM_PAIRVOTE
         // A/B: both row blocks of a column block (one B operand) issued back to back, one max tree
@@ -678,38 +683,30 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         }
 #endif
         mm_f16v accs[2];
-#ifdef MM_PIPE
-        accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[0], (mm_f16v){}, 0, 0, 0);
-#endif
+        if constexpr (PIPE) accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[0], (mm_f16v){}, 0, 0, 0);
 #pragma unroll
         for (int q = 0; q < NQB; ++q) {
           const int kb = q / RB, rb = q - kb * RB;
-#ifdef MM_PIPE
-          if (q + 1 < NQB)
-            accs[(q + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[(q + 1) % RB], bt[(q + 1) / RB],
-                                                                        (mm_f16v){}, 0, 0, 0);
-          const mm_f16v acc = accs[q & 1];
-#else
-          const mm_f16v acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[kb], (mm_f16v){}, 0, 0, 0);
-          (void)accs;
-#endif
+          mm_f16v acc;
+          if constexpr (PIPE) {
+            if (q + 1 < NQB)
+              accs[(q + 1) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[(q + 1) % RB], bt[(q + 1) / RB],
+                                                                          (mm_f16v){}, 0, 0, 0);
+            acc = accs[q & 1];
+          } else {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[rb], bt[kb], (mm_f16v){}, 0, 0, 0);
+          }
           {
             // S' >= +0 <=> its bits are a non-negative int (S' is never NaN; -0 cannot occur with
             // the tau/2 term, and a true candidate has S' > E/2 anyway).  Integer max3 keeps the
             // reads of the MFMA result visible to the compiler's hazard recognizer (an inline-asm
             // v_max3 here read the accumulator before the MFMA had written it).
-#ifdef MM_TREE
-            // A/B: a balanced max3 tree (dependent depth 3 instead of 8)
+            // a balanced max3 tree (dependent depth 3 instead of a chain of 8)
             auto ai = [&](int i) { return __float_as_int(acc[i]); };
             const int m0 = max(max(ai(0), ai(1)), ai(2)), m1 = max(max(ai(3), ai(4)), ai(5));
             const int m2 = max(max(ai(6), ai(7)), ai(8)), m3 = max(max(ai(9), ai(10)), ai(11));
             const int m4 = max(max(ai(12), ai(13)), ai(14));
             const int mx = max(max(max(m0, m1), m2), max(max(m3, m4), ai(15)));
-#else
-            int mx = __float_as_int(acc[0]);
-#pragma unroll
-            for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(acc[i]));
-#endif
 #ifdef MM_DIAG_NOVOTE  // diagnostic timing build only: MFMA + max tree, no vote, no candidates
             if (mx == 0x7fffffff) c_n = 0;
             if (false) {

@@ -126,10 +126,10 @@ struct picp_vo {
   std::vector<char> split_c;          // [chains]
   std::vector<float4*> part_e;        // [chains][2]: early ranges + the late slot, by step parity
   std::vector<int64_t> cap_e;         // [chains]
+  std::vector<int> ks_e;              // [chains]: the early part's range split (PICP_VO_EKS forces)
   std::vector<hipStream_t> estream;   // [chains]
-  std::vector<hipEvent_t> ev_app;     // [chains]: the chain's latest append
+  std::vector<hipEvent_t> ev_app;     // [chains]: the chain's latest merged match
   std::vector<hipEvent_t> ev_early;   // [chains][2]: the early part of step t done (by parity)
-  hipEvent_t ev_boot = nullptr;       // the bootstrap append (step 1's early parts may start)
   float4* part_p = nullptr;
   int64_t cap_p = 0;
   // the step's gather runs inside the PICP block kernel (picp_launch_vo_block) when every frame's
@@ -204,7 +204,6 @@ extern "C" int picp_vo_destroy(picp_vo_t* h) {
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->ev_early)
     if (e) hipEventDestroy(e);
-  if (h->ev_boot) hipEventDestroy(h->ev_boot);
   for (hipStream_t c : h->estream)
     if (c) hipStreamDestroy(c);
   for (hipStream_t c : h->cstream)
@@ -311,13 +310,27 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
       h->estream.assign((size_t)h->chains, nullptr);
       h->ev_app.assign((size_t)h->chains, nullptr);
       h->ev_early.assign((size_t)2 * h->chains, nullptr);
+      // A/B (PICP_VO_ECU_SKIP=k): the early parts on CU-masked queues leaving every k-th CU to
+      // the step chains (a CU-masked stream has the default priority)
+      const char* cm = getenv("PICP_VO_ECU_SKIP");
+      std::vector<uint32_t> mask;
+      if (cm && atoi(cm) >= 2) {
+        int ncu = 0;
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        const int k = atoi(cm);
+        mask.assign((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+          if (i % k != k - 1) mask[(size_t)i / 32] |= 1u << (i % 32);
+      }
       for (int c = 0; c < h->chains; ++c) {
-        HIP_TRY(hipStreamCreateWithPriority(&h->estream[c], hipStreamNonBlocking, lo));
+        if (!mask.empty())
+          HIP_TRY(hipExtStreamCreateWithCUMask(&h->estream[c], (uint32_t)mask.size(), mask.data()));
+        else
+          HIP_TRY(hipStreamCreateWithPriority(&h->estream[c], hipStreamNonBlocking, lo));
         HIP_TRY(hipEventCreateWithFlags(&h->ev_app[c], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h->ev_early[2 * c + 1], hipEventDisableTiming));
       }
-      HIP_TRY(hipEventCreateWithFlags(&h->ev_boot, hipEventDisableTiming));
     }
     return PICP_OK;
   }());
@@ -478,11 +491,16 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   // slot for the late part (2 buffers: step t's merge and step t+2's early part overlap)
   std::vector<char> split_c((size_t)chains_eff, 0);
   std::vector<int64_t> cap_e((size_t)chains_eff, 0);
+  std::vector<int> ks_e((size_t)chains_eff, 1);
+  const char* eks = getenv("PICP_VO_EKS");
   std::vector<Part> p_parte;
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
     split_c[c] = !h->estream.empty() && (h->split_env == 1 || (h->split_env < 0 && ks_w[c] > 1));
-    if (split_c[c]) cap_e[c] = (int64_t)(ks_w[c] + 1) * nsc * std::max<int64_t>(h->max_obs, 1);
+    ks_e[c] = (eks && atoi(eks) > 0) ? std::max(picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only,
+                                                                         atoi(eks)), 1)
+                                     : ks_w[c];
+    if (split_c[c]) cap_e[c] = (int64_t)(ks_e[c] + 1) * nsc * std::max<int64_t>(h->max_obs, 1);
     p_parte.push_back(part((size_t)2 * cap_e[c] * sizeof(float4)));
   }
   // the frame->next launches, as vo_frame_match issues them: the whole table up front (overlap off)
@@ -523,6 +541,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     if (p_partw[c].bytes) h->part_w[c] = (float4*)(m + p_partw[c].off);
   h->split_c = split_c;
   h->cap_e = cap_e;
+  h->ks_e = ks_e;
   h->part_e.assign((size_t)2 * chains_eff, nullptr);
   for (int c = 0; c < chains_eff; ++c)
     if (split_c[c]) {
@@ -702,8 +721,6 @@ static hipError_t vo_enqueue(picp_vo* h) {
   }
   if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(h->stream, &h->vargs, -1);
   const int C = std::min(h->chains_eff, h->n_seg);
-  bool any_split = false;
-  for (int c = 0; c < C; ++c) any_split = any_split || h->split_c[c];
   // step u's early world-match part of chain c (the map as step u-2's append left it) on the
   // chain's early stream; its ranges go to scratch slots 0.. of buffer u & 1
   auto early_part = [&](int c, const VoArgs& V, int u) {
@@ -713,12 +730,12 @@ static hipError_t vo_enqueue(picp_vo* h) {
     if (!(skip & 8))
       r = picp_launch_match_mfma_parts(es, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
                                        V.map_h, V.map_n1, V.map_n2, V.eprobs + (size_t)p * h->n_seg + V.seg0,
-                                       h->dim, VO_MATCH_DIST, VO_MATCH_RATIO, h->accept_only, h->ks_w[c], 0,
+                                       h->dim, VO_MATCH_DIST, VO_MATCH_RATIO, h->accept_only, h->ks_e[c], 0,
                                        h->part_e[2 * c + p], h->cap_e[c]);
     if (r == hipSuccess) r = hipEventRecord(h->ev_early[2 * c + p], es);
     return r;
   };
-  if (e == hipSuccess && any_split) e = hipEventRecord(h->ev_boot, h->stream);
+
   // one world-match launch over chain c's segments [s0, s0 + n): tables probs (+ s0)
   auto world_match = [&](hipStream_t st, const VoArgs& V, const MatchProblem* probs, int c) {
     return picp_launch_match_mfma(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1, V.map_h,
@@ -748,12 +765,7 @@ static hipError_t vo_enqueue(picp_vo* h) {
     for (int s = s0; s < s1; ++s) csteps[c] = std::max(csteps[c], (int)h->segs[s].steps);
     max_steps = std::max(max_steps, csteps[c]);
   }
-  // step 1's early parts: the map the bootstrap left
-  for (int c = 0; c < C && e == hipSuccess; ++c)
-    if (h->split_c[c] && csteps[c] > 1) {
-      e = hipStreamWaitEvent(h->estream[c], h->ev_boot, 0);
-      if (e == hipSuccess) e = early_part(c, cv[c], 1);
-    }
+
   for (int t = 0; t < max_steps && e == hipSuccess; ++t) {
     for (int c = 0; c < C && e == hipSuccess; ++c) {
       if (t >= csteps[c]) continue;
@@ -771,14 +783,22 @@ static hipError_t vo_enqueue(picp_vo* h) {
         if (e == hipSuccess && !(skip & 8))
           e = picp_launch_match_mfma_parts(st, V.n_seg, h->max_obs, h->desc_d, V.map_desc, h->obs_h, h->obs_n1,
                                            V.map_h, V.map_n1, V.map_n2, V.lprobs + s0, h->dim, VO_MATCH_DIST,
-                                           VO_MATCH_RATIO, h->accept_only, 1, h->ks_w[c], h->part_e[2 * c + p],
+                                           VO_MATCH_RATIO, h->accept_only, 1, h->ks_e[c], h->part_e[2 * c + p],
                                            h->cap_e[c]);
         if (e == hipSuccess && !(skip & 8))
-          e = picp_launch_match_merge(st, V.eprobs + (size_t)p * h->n_seg + s0, V.n_seg, h->max_obs, h->ks_w[c],
-                                      h->ks_w[c], h->part_e[2 * c + p], h->cap_e[c], VO_MATCH_DIST, VO_MATCH_RATIO,
+          e = picp_launch_match_merge(st, V.eprobs + (size_t)p * h->n_seg + s0, V.n_seg, h->max_obs, h->ks_e[c],
+                                      h->ks_e[c], h->part_e[2 * c + p], h->cap_e[c], VO_MATCH_DIST, VO_MATCH_RATIO,
                                       h->wm_bi, h->wm_bd, h->wm_sd, h->wm_acc);
       } else if (e == hipSuccess && !(skip & 8)) {
         e = world_match(st, V, h->wprobs_d, c);
+      }
+      // step t+1's early part (the map as step t-1's append left it), started once this step's
+      // match is merged: it runs beside this step's latency-bound PICP kernel and append rather
+      // than beside the next step's late part and merge (round 6, profiles/r06/t15/)
+      if (h->split_c[c] && t + 1 < csteps[c] && e == hipSuccess) {
+        e = hipEventRecord(h->ev_app[c], st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->estream[c], h->ev_app[c], 0);
+        if (e == hipSuccess) e = early_part(c, V, t + 1);
       }
       if (e == hipSuccess && t == 0 && C > 1 && c + 1 < C) e = hipEventRecord(h->ev_ph[c], st);
       if (fused) {
@@ -795,11 +815,6 @@ static hipError_t vo_enqueue(picp_vo* h) {
 #endif
       if (e == hipSuccess && ov && t >= 1) e = hipStreamWaitEvent(st, h->ev_chunk[t], 0);
       if (e == hipSuccess && !(skip & 2)) e = picp_launch_vo_append(st, &V, t);
-      if (h->split_c[c] && t + 2 < csteps[c] && e == hipSuccess) {  // step t+2's early part
-        e = hipEventRecord(h->ev_app[c], st);
-        if (e == hipSuccess) e = hipStreamWaitEvent(h->estream[c], h->ev_app[c], 0);
-        if (e == hipSuccess) e = early_part(c, V, t + 2);
-      }
     }
   }
   for (int c = 1; c < C && e == hipSuccess; ++c) e = hipEventRecord(h->ev_cj[c], cst[c]);
