@@ -244,11 +244,6 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #ifndef MM_RT
 #define MM_RT 256  // reference rows per LDS tile (128: -3.4 % on C5, 512: -7 %; profiles/r01/match_ab.log)
 #endif
-// tiles of references in flight ahead of the one computed (pass 2): 1 or 2
-#ifndef MM_PF
-#define MM_PF 1
-#endif
-static_assert(MM_PF == 1 || MM_PF == 2, "MM_PF: 1 or 2");
 #ifndef MM_PIPE_RB2
 #define MM_PIPE_RB2 1  // 0: the RB = 2 folded loop unpipelined (A/B)
 #endif
@@ -436,10 +431,11 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   const int64_t nr_all = P.nr;
   // fetch tile t0 into registers (chunk tid + k*MM_BLOCK; norm tid + k*MM_BLOCK of the tile's
   // [n1 | n2] block), stash them into buffer b
-  // the stage registers: tile t + 1 in flight while tile t is computed (MM_PF = 2: tiles t + 1 and
-  // t + 2, in two stages whose roles alternate between consecutive tiles)
-  mm_half8 stg[CPT], stg2[CPT];
-  float sn[NPN], sn2[NPN];
+  // the stage registers: tile t + 1 in flight while tile t is computed (a two-deep form, tiles t + 1
+  // and t + 2 in alternating stages, measured equal at the 8e shape and -7 % at the default C5
+  // shape: round 6, profiles/r06/t9/ab.log)
+  mm_half8 stg[CPT];
+  float sn[NPN];
   auto fetch_to = [&](int64_t t0, mm_half8 (&g)[CPT], float (&gn)[NPN]) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -630,8 +626,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       ++c_n;
     }
   };
-  // One tile: fold vote (RAD = 2) and barrier, the fetch MM_PF tiles ahead into stage fs, the
-  // compute on LDS buffer b, then the next tile's stage rs (already in flight) stashed into b ^ 1.
+  // One tile: fold vote (RAD = 2) and barrier, the next tile's fetch into stage fs, the compute
+  // on LDS buffer b, then the stage rs (the same registers: the fetch has landed) into b ^ 1.
   auto tile_step = [&](int64_t t0, int b, mm_half8 (&fs)[CPT], float (&fn)[NPN], mm_half8 (&rs)[CPT],
                        float (&rn)[NPN]) {
     const int buf = b;
@@ -639,7 +635,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     if constexpr (RAD == 2) fold = __syncthreads_or(my_nofold) == 0;
     else __syncthreads();
     const bool more = t0 + MM_RT < nr_all;
-    if (t0 + MM_PF * MM_RT < nr_all) fetch_to(t0 + MM_PF * MM_RT, fs, fn);
+    if (t0 + MM_RT < nr_all) fetch_to(t0 + MM_RT, fs, fn);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
       // the B operands of BT column blocks first (one LDS wait per group, not per block);
@@ -659,29 +655,10 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
         // Round 3 measured that slower (a wave per SIMD lost: 108 -> 131 VGPRs, profiles/r03/mab/);
         // with the balanced max tree below it fits 120 VGPRs (four waves) and the default C5 shape
         // ran 780k -> 799k frames/s (320 -> 313 us per chain step), the 8e partition +0.5 %; at RB = 1
-        // it cost the per-rank shape 1.5 % (profiles/r06/t12/ab.log).
+        // it cost the per-rank shape 1.5 % (profiles/r06/t12/ab.log).  As shipped (RB = 2 only),
+        // against the unpipelined build: default C5 774k -> 794k, 8e 44.9k -> 45.5k, the per-rank
+        // shape (RB = 1) equal (profiles/r06/t18/ab.log, three interleaved repetitions).
         constexpr int NQB = BT * RB;
-#ifdef MM_PAIRVOTE
-        // A/B: both row blocks of a column block (one B operand) issued back to back, one max tree
-        // over the two accumulators and one wave vote for the pair
-        if constexpr (RB == 2) {
-#pragma unroll
-          for (int kb = 0; kb < BT; ++kb) {
-            const mm_f16v a0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[kb], (mm_f16v){}, 0, 0, 0);
-            const mm_f16v a1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[1], bt[kb], (mm_f16v){}, 0, 0, 0);
-            int mx = __float_as_int(a0[0]);
-#pragma unroll
-            for (int i = 1; i < 16; ++i) mx = max(mx, __float_as_int(a0[i]));
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mx = max(mx, __float_as_int(a1[i]));
-            if (__any(mx >= 0)) {
-              push_mask(mm_pack16(mm_mask16_rows(a0)), t0, sg + kb, 0);
-              push_mask(mm_pack16(mm_mask16_rows(a1)), t0, sg + kb, 1);
-            }
-          }
-          continue;
-        }
-#endif
         mm_f16v accs[2];
         if constexpr (PIPE) accs[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(qaf[0], bt[0], (mm_f16v){}, 0, 0, 0);
 #pragma unroll
@@ -761,18 +738,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     if constexpr (RAD == 2) my_nofold = fold_check(0);
     stash(0);
   }
-  if constexpr (MM_PF == 1) {
-    for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += MM_RT, b ^= 1) tile_step(t0, (int)b, stg, sn, stg, sn);
-  } else {
-    // tile 1 into stg before the loop; the stages alternate: tile t's step fills one while the
-    // other (tile t + 1, fetched a step earlier) is stashed
-    if (MM_RT < nr_all) fetch(MM_RT);
-    for (int64_t t0 = 0; t0 < nr_all; t0 += 2 * MM_RT) {
-      tile_step(t0, 0, stg2, sn2, stg, sn);
-      if (t0 + MM_RT >= nr_all) break;
-      tile_step(t0 + MM_RT, 1, stg, sn, stg2, sn2);
-    }
-  }
+  for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += MM_RT, b ^= 1) tile_step(t0, (int)b, stg, sn, stg, sn);
   // expand the lane lists into the per-query lists (the same LDS words): every entry of the wave
   // is read into registers and the reads have completed before the first write
   {

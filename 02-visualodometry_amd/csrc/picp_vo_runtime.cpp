@@ -115,14 +115,18 @@ struct picp_vo {
   std::vector<float4*> part_w;    // [chains]
   std::vector<int64_t> cap_w;     // [chains]: part_w's capacity, float4
   std::vector<std::pair<size_t, int>> ks_p;  // frame->next launch starting at problem .first: split .second
-  // The world match split by map age (PICP_VO_SPLIT; default: the chains whose world match is
-  // range-split, i.e. few segments against long maps).  Step t matches frame f0+t+1 against the map
+  // The world match split by map age (PICP_VO_SPLIT=1; off by default: measured slower at every C5
+  // shape -- 8e 44.5k -> 31.4-32.9k frames/s, the per-rank shape 162k -> 75-77k, the default shape
+  // 797k -> 561k -- because the early parts, running beside the step chains for most of a step,
+  // slow the chains' short kernels: the append 20 -> 40-106 us, the merge 6 -> 40 us
+  // (profiles/r06/t13, t16, t17); neither a smaller early split nor CU-masked early queues helped).
+  // Step t matches frame f0+t+1 against the map
   // after step t-1's append.  The map is append-only, so that is the EARLY part -- the map as step
   // t-2's append left it, which needs nothing from step t-1 and runs on the chain's early stream
   // beside step t-1 -- and the LATE part, the points step t-1's append added.  Only the late part
   // and the merge stay on the chain: the merge kernel folds the early ranges and then the late one,
   // the reference's in-order scan over the whole map (the late indices are the map's: idx0).
-  int split_env = -1;                 // PICP_VO_SPLIT: -1 auto, 0 off, 1 every chain
+  int split_env = 0;                  // PICP_VO_SPLIT: 0 off (default), 1 every chain, -1 auto
   std::vector<char> split_c;          // [chains]
   std::vector<float4*> part_e;        // [chains][2]: early ranges + the late slot, by step parity
   std::vector<int64_t> cap_e;         // [chains]
@@ -267,7 +271,7 @@ extern "C" int picp_vo_create(picp_vo_t** out, int device, int rows, int cols, c
   if (const char* e = getenv("PICP_VO_CHAINS")) h->chains = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("PICP_VO_PHASE")) h->phase = atoi(e) != 0;
   if (const char* e = getenv("PICP_VO_FUSE")) h->fuse = atoi(e) != 0;
-  if (const char* e = getenv("PICP_VO_SPLIT")) h->split_env = atoi(e) != 0 ? 1 : 0;
+  if (const char* e = getenv("PICP_VO_SPLIT")) h->split_env = atoi(e) < 0 ? -1 : (atoi(e) != 0 ? 1 : 0);
   if (!h->graph_env && (h->overlap || h->chains > 1)) h->use_graph = false;
   const size_t no = (size_t)std::max<int64_t>(n_obs, 1);
 #define VO_TRY(expr)              \

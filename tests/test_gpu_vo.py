@@ -270,11 +270,11 @@ def _set_env(monkeypatch, env):
 
 
 def test_vo_split_world_match_bit_identical(native, monkeypatch):
-    """The world match split by map age (PICP_VO_SPLIT; on by default where a chain's world match
-    is range-split: few segments against long maps) -- the early part against the map two appends
-    old on its own stream, the late part against the last append's points, merged on the chain --
-    gives the unsplit schedule's poses, step records and maps bit for bit, in the serial order and
-    the concurrent schedule, run after run."""
+    """The world match split by map age (PICP_VO_SPLIT=1, an opt-in schedule; -1: the chains whose
+    world match is range-split) -- the early part against the map two appends old on its own
+    stream, the late part against the last append's points, merged on the chain -- gives the
+    unsplit schedule's poses, step records and maps bit for bit, in the serial order and the
+    concurrent schedule, run after run."""
     from picp_amd.vo_synth import VOSequence, segments
     n = 601
     s = VOSequence(n, obs_per_frame=2000, seed=3)
@@ -287,6 +287,7 @@ def test_vo_split_world_match_bit_identical(native, monkeypatch):
                 {"PICP_VO_SPLIT": "1", "PICP_VO_OVERLAP": "0", "PICP_VO_CHAINS": "1"},
                 {"PICP_VO_SPLIT": "0", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None},
                 {"PICP_VO_SPLIT": "1", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None},
+                {"PICP_VO_SPLIT": "-1", "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None},
                 {"PICP_VO_SPLIT": None, "PICP_VO_OVERLAP": None, "PICP_VO_CHAINS": None}):
         _set_env(monkeypatch, env)
         outs = _vo_outputs(native, F, s.K, first, steps, boot)
