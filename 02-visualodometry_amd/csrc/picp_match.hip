@@ -255,6 +255,24 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #endif
 // Diagnostic build only (-DPICP_STAMPS): [0] queries through the full-scan fallback, [1] total
 // candidates rescanned, [2] queries, [3] max candidates of a query (tools/match_stats.py).
+// Diagnostic build only (-DMM_TSTAMP): s_memtime phase sums of the folded pass-2 tile loop, lane 0
+// of every wave: [0] fold vote + barrier, [1] next tile's fetch issue, [2] compute, [3] fold check +
+// stash (waits for the fetch), [4] tiles, [5] whole tile loop (tools/r06/match_tstamp.py).
+#ifdef MM_TSTAMP
+__device__ unsigned long long picp_match_tstamp[6];
+extern "C" hipError_t picp_debug_match_tstamp(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_match_tstamp), sizeof(picp_match_tstamp), 0,
+                                     hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(picp_match_tstamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  return e;
+}
+#define MM_TS(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define MM_TS(v) (void)0
+#endif
 #ifdef PICP_STAMPS
 __device__ unsigned long long picp_match_stats[4];
 extern "C" hipError_t picp_debug_match_stats(unsigned long long* out, int reset) {
@@ -442,16 +460,6 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       const int ch = tid + k * MM_BLOCK;
       const int64_t row = min(t0 + ch / (DP / 8), nr_all - 1);
       g[k] = *reinterpret_cast<const mm_half8*>(r_h + (P.r_off + row) * DP + (ch % (DP / 8)) * 8);
-      if constexpr (RAD == 2) {
-        // a row past the end folds to S' = -65504 + tau/2 < 0 (never a candidate): components
-        // zero, -n2s/2 hi = -65504, lo = 0, and its [1, 1] slots zero too -- so a partial tile
-        // takes the folded test instead of the compare
-        if (t0 + ch / (DP / 8) >= nr_all) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            g[k][e] = ((ch % (DP / 8)) * 8 + e == dim) ? (_Float16)-65504.0f : (_Float16)0.0f;
-        }
-      }
     }
 #pragma unroll
     for (int k = 0; k < NPN; ++k) {
@@ -464,20 +472,37 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   // range (n1 <= 60000: finite, safe); each thread checks the n1 norms it fetched
   int my_nofold = 0;
   auto fold_check_of = [&](const float (&gn)[NPN]) {
-    int bad = 0;  // rows past the end are neutralised by fetch (their clamped norms are safe)
+    int bad = 0;  // rows past the end are neutralised by the stash (their clamped norms are safe)
 #pragma unroll
     for (int k = 0; k < NPN; ++k)
       if (tid + k * MM_BLOCK < MM_RT) bad |= (gn[k] <= MM_FOLD_MAX) ? 0 : 1;
     return bad;
   };
   auto fold_check = [&](int64_t) { return fold_check_of(sn); };
-  auto stash_from = [&](int b, const mm_half8 (&g)[CPT], const float (&gn)[NPN]) {
+  // The fetched rows go to LDS as loaded, except (RAD = 2) rows past the end: they fold to
+  // S' = -65504 + tau/2 < 0 (never a candidate): components zero, -n2s/2 hi = -65504, lo = 0, and
+  // its [1, 1] slots zero too -- so a partial tile takes the folded test instead of the compare.
+  // The replacement happens HERE, after the compute, not in the fetch: rewriting the loaded
+  // registers there made every fetch wait for its own data right after issuing it (an
+  // s_waitcnt vmcnt behind the loads, 2,000-7,500 cycles per tile: profiles/r06/t21/tstamp.txt).
+  auto stash_from = [&](int b, int64_t t0, const mm_half8 (&g)[CPT], const float (&gn)[NPN]) {
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) s_t[b][tid + k * MM_BLOCK] = g[k];
+    for (int k = 0; k < CPT; ++k) {
+      const int ch = tid + k * MM_BLOCK;
+      mm_half8 v = g[k];
+      if constexpr (RAD == 2) {
+        if (t0 + ch / (DP / 8) >= nr_all) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = ((ch % (DP / 8)) * 8 + e == dim) ? (_Float16)-65504.0f : (_Float16)0.0f;
+        }
+      }
+      s_t[b][ch] = v;
+    }
 #pragma unroll
     for (int k = 0; k < NPN; ++k) (&s_n[b][0][0])[tid + k * MM_BLOCK] = gn[k];
   };
-  auto stash = [&](int b) { stash_from(b, stg, sn); };
+  auto stash = [&](int b, int64_t t0) { stash_from(b, t0, stg, sn); };
   auto load_b = [&](int b, int col, mm_half8* bb) {
 #pragma unroll
     for (int c = 0; c < KCH; ++c) bb[c] = s_t[b][col * (DP / 8) + 2 * c + hf];
@@ -548,7 +573,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   float rmax = 0.0f;
   if (nr_all > 0) {
     fetch(0);
-    stash(0);
+    stash(0, 0);
   }
   buf = 0;
   for (int64_t t0 = 0; t0 < nr_all; t0 += MM_RT, buf ^= 1) {
@@ -579,7 +604,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
           b1[rb][i] = mm_min3(b1[rb][i], fmaf(-2.0f, acc_a[i], na), fmaf(-2.0f, acc_b[i], nb));
       }
     }
-    if (more) stash(buf ^ 1);
+    if (more) stash(buf ^ 1, t0 + MM_RT);
   }
   // merge the 32 columns of each row (lanes with equal hf): top-2 of the union
 #pragma unroll
@@ -628,14 +653,20 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   };
   // One tile: fold vote (RAD = 2) and barrier, the next tile's fetch into stage fs, the compute
   // on LDS buffer b, then the stage rs (the same registers: the fetch has landed) into b ^ 1.
+#ifdef MM_TSTAMP
+  unsigned long long ts_acc[6] = {0, 0, 0, 0, 0, 0}, ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, tsl0 = 0, tsl1 = 0;
+#endif
   auto tile_step = [&](int64_t t0, int b, mm_half8 (&fs)[CPT], float (&fn)[NPN], mm_half8 (&rs)[CPT],
                        float (&rn)[NPN]) {
     const int buf = b;
     bool fold = false;
+    MM_TS(ts0);
     if constexpr (RAD == 2) fold = __syncthreads_or(my_nofold) == 0;
     else __syncthreads();
+    MM_TS(ts1);
     const bool more = t0 + MM_RT < nr_all;
     if (t0 + MM_RT < nr_all) fetch_to(t0 + MM_RT, fs, fn);
+    MM_TS(ts2);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
       // the B operands of BT column blocks first (one LDS wait per group, not per block);
@@ -702,10 +733,20 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
           }
         }
       }  // column-block group
+      MM_TS(ts3);
       if (more) {
         my_nofold = fold_check_of(rn);  // after the compute: the fetch has landed by now
-        stash_from(buf ^ 1, rs, rn);
+        stash_from(buf ^ 1, t0 + MM_RT, rs, rn);
       }
+#ifdef MM_TSTAMP
+      __builtin_amdgcn_s_waitcnt(0);  // the stash issued and landed
+      MM_TS(ts4);
+      ts_acc[0] += ts1 - ts0;
+      ts_acc[1] += ts2 - ts1;
+      ts_acc[2] += ts3 - ts2;
+      ts_acc[3] += ts4 - ts3;
+      ts_acc[4] += 1;
+#endif
       return;
     }
 #pragma unroll 1
@@ -730,15 +771,22 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     }
     if (more) {
       if constexpr (RAD == 2) my_nofold = fold_check_of(rn);
-      stash_from(buf ^ 1, rs, rn);
+      stash_from(buf ^ 1, t0 + MM_RT, rs, rn);
     }
   };
   if (nr_all > 0) {  // an empty reference set (a late part with no new points): no tile
     fetch(0);
     if constexpr (RAD == 2) my_nofold = fold_check(0);
-    stash(0);
+    stash(0, 0);
   }
+  MM_TS(tsl0);
   for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += MM_RT, b ^= 1) tile_step(t0, (int)b, stg, sn, stg, sn);
+#ifdef MM_TSTAMP
+  MM_TS(tsl1);
+  ts_acc[5] = tsl1 - tsl0;
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&picp_match_tstamp[k], ts_acc[k]);
+#endif
   // expand the lane lists into the per-query lists (the same LDS words): every entry of the wave
   // is read into registers and the reads have completed before the first write
   {
