@@ -244,6 +244,10 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #ifndef MM_RT
 #define MM_RT 256  // reference rows per LDS tile (128: -3.4 % on C5, 512: -7 %; profiles/r01/match_ab.log)
 #endif
+#ifndef MM_PF
+#define MM_PF 1  // tiles of references in flight ahead of the computed one (pass 2): 1, 2 or 3
+#endif
+static_assert(MM_PF >= 1 && MM_PF <= 3, "MM_PF: 1, 2 or 3");
 #ifndef MM_PIPE_RB2
 #define MM_PIPE_RB2 1  // 0: the RB = 2 folded loop unpipelined (A/B)
 #endif
@@ -449,11 +453,10 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   const int64_t nr_all = P.nr;
   // fetch tile t0 into registers (chunk tid + k*MM_BLOCK; norm tid + k*MM_BLOCK of the tile's
   // [n1 | n2] block), stash them into buffer b
-  // the stage registers: tile t + 1 in flight while tile t is computed (a two-deep form, tiles t + 1
-  // and t + 2 in alternating stages, measured equal at the 8e shape and -7 % at the default C5
-  // shape: round 6, profiles/r06/t9/ab.log)
-  mm_half8 stg[CPT];
-  float sn[NPN];
+  // the stage registers: MM_PF tiles in flight while tile t is computed (t + 1 .. t + MM_PF), in
+  // MM_PF stages whose roles rotate from tile to tile (no register moves)
+  mm_half8 stg[CPT], stg2[CPT], stg3[CPT];
+  float sn[NPN], sn2[NPN], sn3[NPN];
   auto fetch_to = [&](int64_t t0, mm_half8 (&g)[CPT], float (&gn)[NPN]) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -665,7 +668,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     else __syncthreads();
     MM_TS(ts1);
     const bool more = t0 + MM_RT < nr_all;
-    if (t0 + MM_RT < nr_all) fetch_to(t0 + MM_RT, fs, fn);
+    if (t0 + MM_PF * MM_RT < nr_all) fetch_to(t0 + MM_PF * MM_RT, fs, fn);
     MM_TS(ts2);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
@@ -780,7 +783,26 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     stash(0, 0);
   }
   MM_TS(tsl0);
-  for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += MM_RT, b ^= 1) tile_step(t0, (int)b, stg, sn, stg, sn);
+  if constexpr (MM_PF == 1) {
+    for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += MM_RT, b ^= 1) tile_step(t0, (int)b, stg, sn, stg, sn);
+  } else if constexpr (MM_PF == 2) {
+    if (MM_RT < nr_all) fetch_to(MM_RT, stg, sn);  // tile 1 in flight
+    for (int64_t t0 = 0; t0 < nr_all; t0 += 2 * MM_RT) {
+      tile_step(t0, 0, stg2, sn2, stg, sn);
+      if (t0 + MM_RT >= nr_all) break;
+      tile_step(t0 + MM_RT, 1, stg, sn, stg2, sn2);
+    }
+  } else {
+    if (MM_RT < nr_all) fetch_to(MM_RT, stg, sn);  // tiles 1 and 2 in flight
+    if (2 * MM_RT < nr_all) fetch_to(2 * MM_RT, stg2, sn2);
+    for (int64_t t0 = 0, b = 0; t0 < nr_all; t0 += 3 * MM_RT, b ^= 1) {
+      tile_step(t0, (int)b, stg3, sn3, stg, sn);
+      if (t0 + MM_RT >= nr_all) break;
+      tile_step(t0 + MM_RT, (int)b ^ 1, stg, sn, stg2, sn2);
+      if (t0 + 2 * MM_RT >= nr_all) break;
+      tile_step(t0 + 2 * MM_RT, (int)b, stg2, sn2, stg3, sn3);
+    }
+  }
 #ifdef MM_TSTAMP
   MM_TS(tsl1);
   ts_acc[5] = tsl1 - tsl0;
