@@ -120,6 +120,18 @@ extern "C" hipError_t picp_launch_vo_gather(hipStream_t stream, const VoArgs* a,
   return hipGetLastError();
 }
 
+#ifdef VOA_TSTAMP
+extern "C" hipError_t picp_debug_voa_tstamp(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(picp_voa_tstamp), sizeof(picp_voa_tstamp), 0,
+                                     hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[5] = {0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(picp_voa_tstamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  return e;
+}
+#endif
+
 extern "C" hipError_t picp_launch_vo_append(hipStream_t stream, const VoArgs* a, int t) {
   if (!a || a->n_seg <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(vo_append_kernel, dim3(a->n_seg), dim3(VOA_BLOCK), 0, stream, *a, t);

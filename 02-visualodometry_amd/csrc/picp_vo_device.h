@@ -6,6 +6,17 @@
 
 namespace picp {
 
+// Diagnostic build only (-DVOA_TSTAMP): s_memrealtime phase sums of the append (thread 0 of every
+// block, steps t >= 0; 100 MHz ticks): [0] record + projections, [1] pass 1 (flags, compaction),
+// [2] pass 2 (triangulate, append; every lane), [3] the next problem and state, [4] blocks
+// (tools/r06/append_tstamp.py).
+#ifdef VOA_TSTAMP
+__device__ unsigned long long picp_voa_tstamp[5];
+#define VOA_TS(v) v = __builtin_amdgcn_s_memrealtime()
+#else
+#define VOA_TS(v) (void)0
+#endif
+
 // Eigen::Isometry3f::inverse() of a column-major 4x4 (oracle/picp_oracle.c or_iso_inverse order)
 __device__ __forceinline__ void vo_iso_inverse(const float* T, float* Ti) {
 #pragma clang fp contract(off)
@@ -81,6 +92,10 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
   const int64_t oc = a.frame_off[cf], nc = a.frame_off[cf + 1] - oc;
   const int64_t on = a.frame_off[nf];
   const int64_t rec = G.slot0 + (boot ? 0 : t + 1);
+#ifdef VOA_TSTAMP
+  unsigned long long vt0 = 0, vt1 = 0, vt2 = 0, vt3 = 0, vt4 = 0;
+#endif
+  VOA_TS(vt0);
   if (threadIdx.x == 0) {
     float Tp[16], Te[16];
     if (boot) {
@@ -130,6 +145,7 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
     for (int k = 0; k < 16; ++k) sTn[k] = boot ? Tp[k] : Te[k];
   }
   __syncthreads();
+  VOA_TS(vt1);
   const int64_t mbase = G.map_off + s_base;
   const int dim = a.dim;
   int2* pairs = a.pairs + (int64_t)s * a.cap_c;
@@ -170,6 +186,7 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
     cnt += tot;
   }
   __syncthreads();
+  VOA_TS(vt2);
   // pass 2: every lane triangulates (src/cam.cpp:115-139) and appends (xyz, curr descriptor)
   for (int64_t k = threadIdx.x; k < cnt; k += NT) {
     const int2 pr = pairs[k];
@@ -201,6 +218,10 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
     a.map_n1[slot] = n1;
     a.map_n2[slot] = n2;
   }
+#ifdef VOA_TSTAMP
+  __syncthreads();
+#endif
+  VOA_TS(vt3);
   if (threadIdx.x == 0) {
     const int64_t mn = s_base + cnt;
     a.map_n[s] = mn;
@@ -244,6 +265,16 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
 #pragma unroll
     for (int i = 0; i < 3; ++i) st.t[i] = Twc[12 + i];
     a.st_in[s] = st;
+#ifdef VOA_TSTAMP
+    VOA_TS(vt4);
+    if (!boot) {
+      atomicAdd(&picp_voa_tstamp[0], vt1 - vt0);
+      atomicAdd(&picp_voa_tstamp[1], vt2 - vt1);
+      atomicAdd(&picp_voa_tstamp[2], vt3 - vt2);
+      atomicAdd(&picp_voa_tstamp[3], vt4 - vt3);
+      atomicAdd(&picp_voa_tstamp[4], 1ull);
+    }
+#endif
   }
 }
 
