@@ -160,6 +160,7 @@ typedef float mm_f16v __attribute__((ext_vector_type(16)));
 // MM_KMIN (so a range is worth a block's query prologue), whole tiles; mm_nsplit non-empty ranges.
 #define MM_KMIN 1024
 #define MM_KSPLIT_MAX 16        // the occupancy split's cap (picp_match_ksplit)
+#define MM_KSPLIT_MAX2 32       // ... for the folded form at two row blocks per wave
 #define MM_KSPLIT_LIMIT 65536   // a launch's hard limit (reference sets up to 2^36 rows in 2^20-row ranges)
 __host__ __device__ __forceinline__ int64_t mm_kchunk(int64_t nr, int ksplit) {
   const int64_t c = (nr + ksplit - 1) / ksplit;
@@ -1142,6 +1143,16 @@ extern "C" int picp_match_ksplit_forced(int n_problems, int64_t max_nq, int64_t 
   const int64_t base = (int64_t)n_problems * ((max_nq + 32 * MM_WAVES - 1) / (32 * MM_WAVES));
   int64_t k = (4 * (int64_t)num_cu + base - 1) / std::max<int64_t>(base, 1);
   k = std::max<int64_t>(1, std::min<int64_t>(k, MM_KSPLIT_MAX));
+  // The folded accept-only form (form bits 0 and 2: the caller's dim <= 12) with few problems runs
+  // two row blocks per wave (the launcher's RB rule): there, as many ranges as fill ONE generation
+  // of four RB = 2 blocks per CU, up to 32, when every range keeps >= 4,096 rows.  The 8e world
+  // match: 4 problems x 9 query blocks x 28 ranges = 1,008 blocks instead of 16 ranges' 576, C5 8e
+  // +2.2 % (46.3k / 45.9k -> 47.4k / 46.8k frames/s; 24 ranges equal, 32 -1 %: profiles/r06/t26/).
+  if ((form & 1) && (form & 4)) {
+    const int64_t b2 = (int64_t)n_problems * ((max_nq + 64 * MM_WAVES - 1) / (64 * MM_WAVES));
+    const int64_t k2 = (4 * (int64_t)num_cu) / std::max<int64_t>(b2, 1);
+    if (k2 >= 8 && max_nr >= k2 * 4096) k = std::min<int64_t>(k2, MM_KSPLIT_MAX2);
+  }
   if (force > 0) k = std::min<int64_t>(force, MM_KSPLIT_LIMIT);  // an A/B count may pass the cap
   // the entries' range: split the largest set at least that far (beyond the occupancy cap)
   const int64_t k_range = (max_nr + ((int64_t)MM_RT << 12) - 1) / ((int64_t)MM_RT << 12);

@@ -1557,7 +1557,8 @@ extern "C" int picp_match_batch_form(int device, int n_problems, const int64_t* 
   // the reference-range split's scratch (picp_match_ksplit: few problems against many references)
   int64_t max_nr = 0;
   for (const MatchProblem& q : probs) max_nr = std::max(max_nr, q.nr);
-  const int ks = picp_match_ksplit(n_problems, max_nq, max_nr, form);
+  // (form bit 2 for the split rule: the folded form needs dim <= 12)
+  const int ks = picp_match_ksplit(n_problems, max_nq, max_nr, form | (dim <= 12 ? 4 : 0));
   const int64_t part_cap = picp_match_split_scratch(ks, n_problems, max_nq);
   const size_t b_part = (size_t)part_cap * sizeof(float4);
   char* buf = nullptr;

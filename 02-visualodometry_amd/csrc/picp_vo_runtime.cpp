@@ -482,12 +482,14 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   const Part p_mn2 = part((size_t)map_slots * sizeof(float));
   // split scratch: each chain's world match (its n_seg_c problems) and the frame->next launches
   const int ks_force = picp_match_ksplit_env();
+  // the split rule's form: the folded accept-only form needs dim <= 12 (bit 2)
+  const int ks_form = h->accept_only | (h->dim <= 12 ? 4 : 0);
   std::vector<int> ks_w((size_t)chains_eff, 1);
   std::vector<int64_t> cap_w((size_t)chains_eff, 0);
   std::vector<Part> p_partw;
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
-    ks_w[c] = picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only, ks_force);
+    ks_w[c] = picp_match_ksplit_forced(nsc, h->max_obs, max_map, ks_form, ks_force);
     cap_w[c] = picp_match_split_scratch(ks_w[c], nsc, h->max_obs);
     p_partw.push_back(part((size_t)cap_w[c] * sizeof(float4)));
   }
@@ -501,7 +503,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
   for (int c = 0; c < chains_eff; ++c) {
     const int nsc = (int)((int64_t)n_seg * (c + 1) / chains_eff - (int64_t)n_seg * c / chains_eff);
     split_c[c] = !h->estream.empty() && (h->split_env == 1 || (h->split_env < 0 && ks_w[c] > 1));
-    ks_e[c] = (eks && atoi(eks) > 0) ? std::max(picp_match_ksplit_forced(nsc, h->max_obs, max_map, h->accept_only,
+    ks_e[c] = (eks && atoi(eks) > 0) ? std::max(picp_match_ksplit_forced(nsc, h->max_obs, max_map, ks_form,
                                                                          atoi(eks)), 1)
                                      : ks_w[c];
     if (split_c[c]) cap_e[c] = (int64_t)(ks_e[c] + 1) * nsc * std::max<int64_t>(h->max_obs, 1);
@@ -515,7 +517,7 @@ extern "C" int picp_vo_set_segments(picp_vo_t* h, int n_seg, const int64_t* firs
     auto plan = [&](size_t p0, size_t p1) {
       for (size_t q = p0; q < p1; q += VO_MAX_GRID_Y) {
         const int n = (int)std::min<size_t>(VO_MAX_GRID_Y, p1 - q);
-        const int k = picp_match_ksplit_forced(n, h->max_obs, h->max_obs, h->accept_only, ks_force);
+        const int k = picp_match_ksplit_forced(n, h->max_obs, h->max_obs, ks_form, ks_force);
         ks_p.emplace_back(q, k);
         cap_p = std::max(cap_p, picp_match_split_scratch(k, n, h->max_obs));
       }
