@@ -163,14 +163,34 @@ __device__ __forceinline__ void vo_append_body(const VoArgs& a, int t, int s, co
 #pragma unroll
   for (int c = 0; c < PF; ++c)  // next point not among the map correspondences
     fl[c] = fl[c] && (boot || a.wm_acc[on + (fl[c] ? jb[c] : 0)] == 0);
-  // ... then the ordered compaction from registers
+  // ... then the ordered compaction of every chunk with ONE barrier (vo_gather_items' form): per
+  // (chunk, wave) counts, then each flagged pair's index = flagged before its chunk + before its
+  // wave + its lane rank -- the order of the per-chunk compaction (two barriers per chunk) it replaces
+  // (the same bits; C5 within +-0.5 % at every shape, profiles/r06/t29/ab.log)
+  {
+    __shared__ int s_wc[PF][NW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int rk[PF];
 #pragma unroll
-  for (int c = 0; c < PF; ++c) {
-    if ((int64_t)c * NT >= nc) break;  // uniform
-    int tot;
-    const int r = vo_block_rank<NW>(fl[c], s_cnt, &tot);
-    if (fl[c]) pairs[cnt + r] = make_int2(c * NT + (int)threadIdx.x, jb[c]);
-    cnt += tot;
+    for (int c = 0; c < PF; ++c) {
+      const unsigned long long m = __ballot(fl[c]);
+      rk[c] = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) s_wc[c][w] = __popcll(m);
+    }
+    __syncthreads();
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < PF; ++c) {
+      int pre = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        pre += (k < w) ? s_wc[c][k] : 0;
+        tot += s_wc[c][k];
+      }
+      if (fl[c]) pairs[n + pre + rk[c]] = make_int2(c * NT + (int)threadIdx.x, jb[c]);
+      n += tot;
+    }
+    cnt = n;
   }
   for (int64_t c0 = (int64_t)PF * NT; c0 < nc; c0 += NT) {  // frames > 4096 obs
     const int64_t i = c0 + threadIdx.x;
