@@ -386,6 +386,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     mm_half8 t[2][CH];                   // tile rows, 16-B chunks: row*(DP/8) + c*2 + h
     float n[2][2][MM_RT];                // [buf][n1|n2][ref]
     int cnt[MM_WAVES][QPW];
+    int nofold[2];  // RAD = 2: 1 + the index of the tile in LDS buffer b that holds an unsafe reference
     int list[MM_WAVES][QPW][MM_CAP];
     float nq[MM_WAVES][QPW];
   };
@@ -449,6 +450,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     if (RAD == 2 && !(nq <= MM_FOLD_MAX)) nq = INFINITY;  // outside the fold's range: full scan
     s_nq[w][lane] = nq;
     s_cnt[w][lane] = 0;
+    if (tid < 2) lds.nofold[tid] = 0;  // ordered before the first stash by the barrier below
   }
 
   const int64_t nr_all = P.nr;
@@ -474,7 +476,10 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
   auto fetch = [&](int64_t t0) { fetch_to(t0, stg, sn); };
   // RAD = 2: a tile is folded iff it is whole and every reference in it is inside the fold's
   // range (n1 <= 60000: finite, safe); each thread checks the n1 norms it fetched
-  int my_nofold = 0;
+  // (RAD = 2: whether a tile folds travels with it through LDS: the stash tags its buffer with the
+  // tile's index when a fetched norm is unsafe, and the tile loop's one barrier orders the tag before
+  // the read -- a block-wide OR vote cost three barriers per tile, 634-826 cycles per wave and tile:
+  // profiles/r06/t22/tstamp.txt)
   auto fold_check_of = [&](const float (&gn)[NPN]) {
     int bad = 0;  // rows past the end are neutralised by the stash (their clamped norms are safe)
 #pragma unroll
@@ -665,8 +670,8 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     const int buf = b;
     bool fold = false;
     MM_TS(ts0);
-    if constexpr (RAD == 2) fold = __syncthreads_or(my_nofold) == 0;
-    else __syncthreads();
+    __syncthreads();
+    if constexpr (RAD == 2) fold = lds.nofold[b] != (int)(t0 / MM_RT) + 1;
     MM_TS(ts1);
     const bool more = t0 + MM_RT < nr_all;
     if (t0 + MM_PF * MM_RT < nr_all) fetch_to(t0 + MM_PF * MM_RT, fs, fn);
@@ -739,7 +744,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       }  // column-block group
       MM_TS(ts3);
       if (more) {
-        my_nofold = fold_check_of(rn);  // after the compute: the fetch has landed by now
+        if (fold_check_of(rn)) lds.nofold[buf ^ 1] = (int)(t0 / MM_RT) + 2;  // the fetch has landed by now
         stash_from(buf ^ 1, t0 + MM_RT, rs, rn);
       }
 #ifdef MM_TSTAMP
@@ -774,13 +779,17 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       }
     }
     if (more) {
-      if constexpr (RAD == 2) my_nofold = fold_check_of(rn);
+      if constexpr (RAD == 2)
+        if (fold_check_of(rn)) lds.nofold[buf ^ 1] = (int)(t0 / MM_RT) + 2;
       stash_from(buf ^ 1, t0 + MM_RT, rs, rn);
     }
   };
   if (nr_all > 0) {  // an empty reference set (a late part with no new points): no tile
     fetch(0);
-    if constexpr (RAD == 2) my_nofold = fold_check(0);
+    if constexpr (RAD == 2) {
+      __syncthreads();  // the tags' initialisation before the first one is set
+      if (fold_check(0)) lds.nofold[0] = 1;
+    }
     stash(0, 0);
   }
   MM_TS(tsl0);
