@@ -249,6 +249,11 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #define MM_PF 1  // tiles of references in flight ahead of the computed one (pass 2): 1, 2 or 3
 #endif
 static_assert(MM_PF >= 1 && MM_PF <= 3, "MM_PF: 1, 2 or 3");
+#ifndef MM_EARLY
+#define MM_EARLY 0  // 1: the next tile's fetch issued at the previous step's end (PF = 1; A/B:
+                    // equal at every C5 shape, profiles/r06/t35/ab.log)
+#endif
+static_assert(!MM_EARLY || MM_PF == 1, "MM_EARLY needs MM_PF = 1");
 #ifndef MM_PIPE_RB2
 #define MM_PIPE_RB2 1  // 0: the RB = 2 folded loop unpipelined (A/B)
 #endif
@@ -674,7 +679,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
     if constexpr (RAD == 2) fold = lds.nofold[b] != (int)(t0 / MM_RT) + 1;
     MM_TS(ts1);
     const bool more = t0 + MM_RT < nr_all;
-    if (t0 + MM_PF * MM_RT < nr_all) fetch_to(t0 + MM_PF * MM_RT, fs, fn);
+    if (!MM_EARLY && t0 + MM_PF * MM_RT < nr_all) fetch_to(t0 + MM_PF * MM_RT, fs, fn);
     MM_TS(ts2);
     if (RAD == 2 && fold) {
       // folded radius test: element i of the accumulator is S' of (row i, column col)
@@ -746,6 +751,9 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       if (more) {
         if (fold_check_of(rn)) lds.nofold[buf ^ 1] = (int)(t0 / MM_RT) + 2;  // the fetch has landed by now
         stash_from(buf ^ 1, t0 + MM_RT, rs, rn);
+        // MM_EARLY: the tile after next into the stage just freed, before this step's end (and the
+        // next step's barrier) rather than after that barrier
+        if (MM_EARLY && t0 + 2 * MM_RT < nr_all) fetch_to(t0 + 2 * MM_RT, fs, fn);
       }
 #ifdef MM_TSTAMP
       __builtin_amdgcn_s_waitcnt(0);  // the stash issued and landed
@@ -782,6 +790,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       if constexpr (RAD == 2)
         if (fold_check_of(rn)) lds.nofold[buf ^ 1] = (int)(t0 / MM_RT) + 2;
       stash_from(buf ^ 1, t0 + MM_RT, rs, rn);
+      if (MM_EARLY && t0 + 2 * MM_RT < nr_all) fetch_to(t0 + 2 * MM_RT, fs, fn);
     }
   };
   if (nr_all > 0) {  // an empty reference set (a late part with no new points): no tile
@@ -791,6 +800,7 @@ __global__ __launch_bounds__(MM_BLOCK, MM_MINB) void picp_match_mfma_kernel(
       if (fold_check(0)) lds.nofold[0] = 1;
     }
     stash(0, 0);
+    if (MM_EARLY && MM_RT < nr_all) fetch(MM_RT);
   }
   MM_TS(tsl0);
   if constexpr (MM_PF == 1) {
