@@ -195,6 +195,26 @@ def test_match_reference_range_split(native, oracle, monkeypatch, ksplit, rb):
         _eq(got, oracle.match_points(d1_, d2_))
 
 
+@pytest.mark.parametrize("ksplit", ["1", "3"])
+def test_match_unsafe_tiles_two_row_blocks(native, oracle, monkeypatch, ksplit):
+    """Tiles holding an unsafe reference (|x|^2 > 60000, beyond fp16 range, NaN) between whole safe
+    tiles, at two row blocks per wave and with a range split: the accept-only form decides per
+    tile between the folded test and the compare (the decision travels with the tile through LDS
+    since round 6), the other forms take their own paths; the last tile is partial."""
+    monkeypatch.setenv("PICP_MATCH_RB", "2")
+    monkeypatch.setenv("PICP_MATCH_KSPLIT", ksplit)
+    rng = np.random.default_rng(99)
+    d2 = rng.uniform(-1, 1, (4 * 1024 + 37, 10)).astype(np.float32)
+    d2[300] = 100.0                      # |r|^2 = 1e5 inside fp16 range (tile 1)
+    d2[1500, 4] = 1e6                    # beyond fp16 range (tile 5)
+    d2[2900, 0] = np.nan                 # non-finite (tile 11)
+    d2[4100] = d2[4099]                  # a tie in the partial last tile
+    d1 = np.concatenate([d2[[299, 301, 1499, 1501, 2899, 2901, 4099, 4100, 0]] + 0.0,
+                         d2[rng.choice(len(d2), 300, replace=False)] + rng.normal(0, 0.01, (300, 10)).astype(np.float32),
+                         rng.uniform(-1, 1, (200, 10)).astype(np.float32)])
+    _eq(native.match_points(d1, d2), oracle.match_points(d1, d2))
+
+
 def test_match_past_2_24_references(native, oracle):
     """A reference set past 2^24 rows: the candidate entries index 2^20 references per
     range, so picp_match_ksplit splits such a set into more than MM_KSPLIT_MAX (16) ranges rather
