@@ -249,6 +249,10 @@ extern "C" __global__ void picp_match_prep_kernel(const float* __restrict__ desc
 #define MM_PF 1  // tiles of references in flight ahead of the computed one (pass 2): 1, 2 or 3
 #endif
 static_assert(MM_PF >= 1 && MM_PF <= 3, "MM_PF: 1, 2 or 3");
+#ifndef MM_MERGE32
+#define MM_MERGE32 0  // 1: splits of 17-32 ranges merged in one 32-range chunk (A/B: 8e equal or
+                      // slower than two 16-range chunks, profiles/r06/t37/ab.log)
+#endif
 #ifndef MM_EARLY
 #define MM_EARLY 0  // 1: the next tile's fetch issued at the previous step's end (PF = 1; A/B:
                     // equal at every C5 shape, profiles/r06/t35/ab.log)
@@ -1008,11 +1012,16 @@ static hipError_t mm_merge(hipStream_t stream, const MatchProblem* probs, int n_
                            int extra, const float4* part, float dist_thr, float ratio_thr, int32_t* best_idx,
                            float* best_dist, float* second_dist, int32_t* accepted) {
   const dim3 mg((unsigned)((max_nq + 255) / 256), (unsigned)n_problems);
-  if (ksplit + (extra >= 0 ? 1 : 0) <= 4)
+  // (MM_MERGE32: the ranges in one chunk wherever they fit 32 -- measured no faster)
+  const int nr = ksplit + (extra >= 0 ? 1 : 0);
+  if (nr <= 4)
     hipLaunchKernelGGL(picp_match_merge_kernel<4>, mg, dim3(256), 0, stream, probs, n_problems, ksplit, part, max_nq,
                        dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, extra);
-  else
+  else if (nr <= 16 || MM_MERGE32 == 0)
     hipLaunchKernelGGL(picp_match_merge_kernel<16>, mg, dim3(256), 0, stream, probs, n_problems, ksplit, part, max_nq,
+                       dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, extra);
+  else
+    hipLaunchKernelGGL(picp_match_merge_kernel<32>, mg, dim3(256), 0, stream, probs, n_problems, ksplit, part, max_nq,
                        dist_thr, ratio_thr, best_idx, best_dist, second_dist, accepted, extra);
   return hipGetLastError();
 }
