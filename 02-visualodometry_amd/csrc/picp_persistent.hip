@@ -125,7 +125,7 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
     const float* __restrict__ U, const float* __restrict__ V, const PicpArgs A,
     const PicpState* __restrict__ st_in, PicpState* __restrict__ st_out,
     unsigned long long* gpart, unsigned long long* gpose, unsigned int* err, unsigned int* tagbase,
-    unsigned long long timeout_ticks) {
+    unsigned long long* arrive, unsigned long long timeout_ticks) {
   __shared__ double s_red[PICP_NPART][BS / 64];  // term-major: one row per combining lane
   __shared__ float s_tot[PICP_NPART];
   __shared__ float s_wave[BS / 64][PICP_NPART];
@@ -160,6 +160,15 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
   // and no memset node has to clear the granules before each launch.
   gu32_t* tbase_p = ((gu32_t*)tagbase) + p;
   const unsigned tbase = __hip_atomic_load(tbase_p, RLX_AGENT);
+#ifdef PICP_ARRIVAL
+  // A/B: a per-problem count of block publishes, on a line of its own.  It
+  // tracks tbase * nblk across launches (both zeroed together by the host), so round e is complete
+  // at (tbase + e) * nblk.  The solvers wait on it before the sweep -- a hint only: the sweep
+  // still checks every granule's tag, so a late or reordered count costs time, never a result.
+  gu64_t* arrive_p = ((gu64_t*)arrive) + (size_t)p * 16;
+#else
+  (void)arrive;
+#endif
 
   // this block's slice, loaded once into registers (coalesced: item = tid + k*BLOCK)
   float xs[NPT], ys[NPT], zs[NPT], us[NPT], vs[NPT];
@@ -257,10 +266,20 @@ __global__ __launch_bounds__(BS) void picp_persistent_kernel(
 #pragma unroll
       for (int w = 1; w < BS / 64; ++w) sum += s_wave[w][tid];
       __hip_atomic_store(my_part0 + (epoch & 1) * part_stride + tid, granule(tbase + epoch, sum), RLX_AGENT);
+#ifdef PICP_ARRIVAL
+      if (tid == 0) __hip_atomic_fetch_add(arrive_p, 1ull, RLX_AGENT);  // after wave 0's granule stores
+#endif
     }
     PSTAMP(1);
 
     if (solver) {
+#ifdef PICP_ARRIVAL
+      {
+        const unsigned long long target = (unsigned long long)(tbase + epoch) * (unsigned)nblk;
+        while (__hip_atomic_load(arrive_p, RLX_AGENT) < target && !timed_out(deadline)) {
+        }
+      }
+#endif
       // ---- 2. sweep the problem's partials: 16-B sc1 loads of granule pairs (2c, 2c+1) of
       //         blocks g + NG*i (c = tid&15, g = tid>>4); each 8-B half carries its own tag ----
       const int c = tid & 15, g = tid >> 4;
@@ -574,13 +593,13 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              const PicpState* st_in, PicpState* st_out,
                                              unsigned long long* gpart, unsigned long long* gpose,
                                              unsigned int* err, unsigned int* tagbase,
-                                             unsigned long long timeout_ticks) {
+                                             unsigned long long* arrive, unsigned long long timeout_ticks) {
   if (grid <= 0 || !args || !args->uniform || args->nblk_u > PICP_MAX_PBLK) return hipErrorInvalidValue;
   const int var = picp_variant(args->K, args->keep_outliers);
 #define PICP_LAUNCH_PV(N, PV)                                                                      \
   hipLaunchKernelGGL((picp_persistent_kernel<PShape<N>::npt, PV, PShape<N>::bs>), dim3(grid),      \
                      dim3(PShape<N>::bs), 0, stream, X, Y, Z, U, V, *args, st_in, st_out, gpart, gpose, \
-                     err, tagbase, timeout_ticks)
+                     err, tagbase, arrive, timeout_ticks)
 #define PICP_LAUNCH_P(N)                                                            \
   if (var == PICP_V_PINHOLE) PICP_LAUNCH_PV(N, PICP_V_PINHOLE);                     \
   else if (var == PICP_V_PINHOLE_KEEP) PICP_LAUNCH_PV(N, PICP_V_PINHOLE_KEEP);      \

@@ -34,7 +34,7 @@ extern "C" hipError_t picp_launch_persistent(hipStream_t stream, int grid, int n
                                              const PicpState* st_in, PicpState* st_out,
                                              unsigned long long* gpart, unsigned long long* gpose,
                                              unsigned int* err, unsigned int* tagbase,
-                                             unsigned long long timeout_ticks);
+                                             unsigned long long* arrive, unsigned long long timeout_ticks);
 extern "C" hipError_t picp_launch_block(hipStream_t stream, int n_problems, int npt, const float* X,
                                         const float* Y, const float* Z, const float* U,
                                         const float* V, const PicpArgs* args,
@@ -458,7 +458,7 @@ static int batch_layout(picp_batch* b, const int64_t* offs_in, int np) {
     const int64_t sgrid = xg_grid(b);
     b->sync_bytes = (b->mode == PICP_MODE_PERSISTENT)
                         ? (size_t)round_up(128 + (int64_t)np * PICP_POSE_SETS * PICP_POSE_GRAN * 8 + 2 * (int64_t)nblk * PICP_NPART * 8 +
-                                               (int64_t)np * 4, 256)
+                                               round_up((int64_t)np * 4, 128) + (int64_t)np * 128, 256)
                         : (size_t)round_up(128 + 2 * sgrid * 64 * 8 + sgrid * 4, 256);
     if (b->sync_bytes > b->sync_cap) {
       if (b->sync) hipFree(b->sync);
@@ -605,8 +605,12 @@ static hipError_t enqueue_solve(picp_batch* b, int R) {
     unsigned long long* gpose = reinterpret_cast<unsigned long long*>(b->sync + 128);
     unsigned long long* gpart = gpose + (size_t)b->np * PICP_POSE_SETS * PICP_POSE_GRAN;
     unsigned int* tagbase = reinterpret_cast<unsigned int*>(gpart + 2 * (size_t)b->nblk * PICP_NPART);
+    // per-problem arrival counters on lines of their own, zeroed with the tag bases (A/B builds with
+    // -DPICP_ARRIVAL count the blocks' publishes there; the shipped kernel does not touch them)
+    unsigned long long* arrive =
+        reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(tagbase) + round_up((int64_t)b->np * 4, 128));
     return picp_launch_persistent(b->stream, b->nblk, b->npt, b->X(), b->Y(), b->Z(), b->U(), b->V(),
-                                  &b->args, b->init_d, b->st_d[0], gpart, gpose, err, tagbase,
+                                  &b->args, b->init_d, b->st_d[0], gpart, gpose, err, tagbase, arrive,
                                   b->timeout_ticks);
   }
   hipError_t e = graph_prologue(b);
